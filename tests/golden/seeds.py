@@ -1,0 +1,319 @@
+"""Seeded input builders shared by gen_golden.py and the tests.
+
+TEST INFRASTRUCTURE ONLY.  Every fixture in tests/golden/ was produced from the
+inputs these functions build; the tests rebuild the same inputs from the same
+seeds (torch CPU Generator / numpy RandomState are deterministic for a fixed
+torch/numpy build, and the GPU box runs the same image).
+"""
+import types
+
+import numpy as np
+import torch
+
+
+def _g(seed):
+    g = torch.Generator()
+    g.manual_seed(seed)
+    return g
+
+
+# --------------------------------------------------------------------------
+# R1 renderer cases (utils/process.py:252-278)
+# --------------------------------------------------------------------------
+def render_cases():
+    rs = np.random.RandomState(11)
+    cases = {}
+    k = np.zeros((16, 3), np.float32)
+    k[:, 0] = rs.randint(0, 256, 16)
+    k[:, 1] = rs.randint(0, 256, 16)
+    k[:, 2] = 1.0
+    k[3, :2] += 0.7   # fractional coordinates are truncated
+    k[5, 2] = 0.0     # unlabeled keypoint keeps vis 0
+    k[7] = [0.0, 0.0, 0.0]  # unlabeled row as the datasets emit it
+    cases["mixed16"] = (k, (3, 256, 256), 256, 64)
+
+    e = np.array([[2, 100, 1], [3, 100, 1], [251, 100, 1], [252, 100, 1],
+                  [100, 2, 1], [100, 3, 1], [100, 251, 1], [100, 252, 1],
+                  [255, 255, 1], [256, 10, 1], [-0.5, 50, 1], [3.9, 3.9, 1],
+                  [251.9, 251.9, 1], [-3.7, -3.7, 1], [128.5, 127.25, 1], [64, 64, 0.5]],
+                 np.float32)
+    cases["edges16"] = (e, (3, 256, 256), 256, 64)
+
+    k17 = np.zeros((17, 3), np.float32)
+    k17[:, 0] = rs.uniform(-10, 266, 17)
+    k17[:, 1] = rs.uniform(-10, 266, 17)
+    k17[:, 2] = (rs.uniform(0, 1, 17) > 0.2).astype(np.float32)
+    cases["rand17"] = (k17, (3, 256, 256), 256, 64)
+
+    k384 = np.zeros((16, 3), np.float32)
+    k384[:, 0] = rs.randint(0, 384, 16)
+    k384[:, 1] = rs.randint(0, 384, 16)
+    k384[:, 2] = 1.0
+    cases["res384"] = (k384, (3, 384, 384), 384, 96)
+
+    # non-square image shape exercises the h/w split of the visibility test
+    kr = np.array([[10, 10, 1], [300, 100, 1], [100, 200, 1], [200, 250, 1]], np.float32)
+    cases["rect"] = (kr, (3, 256, 320), 256, 64)
+    return cases
+
+
+# --------------------------------------------------------------------------
+# L1-L7 loss cases
+# --------------------------------------------------------------------------
+def loss_cases():
+    return {
+        "small": dict(B=4, S=2, K=16, R=16, thr=0.95, pw=1.0, lab=[0, 0, 1, 1], seed=101, nlab_feat=2),
+        "r64": dict(B=4, S=2, K=16, R=64, thr=0.95, pw=1.0, lab=[0, 0, 1, 1], seed=102, nlab_feat=2),
+        "s1": dict(B=3, S=1, K=5, R=8, thr=0.5, pw=0.5, lab=[1, 0, 1], seed=103, nlab_feat=2),
+        "s4k17": dict(B=2, S=4, K=17, R=16, thr=0.8, pw=2.0, lab=[0, 1], seed=104, nlab_feat=1),
+        "alllab": dict(B=2, S=2, K=4, R=8, thr=0.95, pw=1.0, lab=[1, 1], seed=105, nlab_feat=2, pseudo=False),
+    }
+
+
+def _blobs(g, shape, R, amp_lo, amp_hi):
+    """Gaussian blobs of random amplitude + small noise: maxima straddle the threshold."""
+    n = int(np.prod(shape))
+    cx = torch.rand(n, generator=g) * (R - 1)
+    cy = torch.rand(n, generator=g) * (R - 1)
+    amp = amp_lo + (amp_hi - amp_lo) * torch.rand(n, generator=g)
+    yy, xx = torch.meshgrid(torch.arange(R, dtype=torch.float32), torch.arange(R, dtype=torch.float32),
+                            indexing="ij")
+    sig = max(R / 16.0, 1.0)
+    d2 = (xx[None] - cx[:, None, None]) ** 2 + (yy[None] - cy[:, None, None]) ** 2
+    v = amp[:, None, None] * torch.exp(-d2 / (2 * sig * sig))
+    v = v + 0.03 * torch.randn(n, R, R, generator=g)
+    return v.reshape(*shape, R, R).contiguous()
+
+
+def loss_inputs(B, S, K, R, thr, pw, lab, seed, nlab_feat, pseudo=True):
+    g = _g(seed)
+    preds = _blobs(g, (B, S, K), R, 0.6, 1.25)
+    gts = _blobs(g, (B, K), R, 0.9, 1.0).clamp(min=0)
+    t0 = _blobs(g, (B, S, K), R, 0.85, 1.35)
+    teachers = torch.stack([t0, t0 + 0.02 * torch.randn(t0.shape, generator=g)]).contiguous()
+    isl = torch.tensor(lab, dtype=torch.bool)
+    gate = (torch.rand(B, K, generator=g) > 0.25).float() * isl.float()[:, None]
+    islf = isl.float()
+    sw_lab = islf[:, None].clone()                                   # projects/tools.py:13
+    sw_nega = torch.where(isl, torch.zeros(B), pw * torch.ones(B))[:, None]   # tools.py:21
+    sw_cons = torch.where(isl, torch.ones(B), pw * torch.ones(B))[:, None]    # tools.py:47
+    C, h = 8, 4
+    f1 = torch.randn(nlab_feat, S, C, h, h, generator=g)
+    f2 = 0.5 * f1 + torch.randn(nlab_feat, S, C, h, h, generator=g)
+    return dict(preds=preds, gts=gts, teachers=teachers, tlast=teachers[:, :, -1].contiguous(),
+                gate=gate, islabeled=isl, sw_lab=sw_lab, sw_nega=sw_nega, sw_cons=sw_cons, f1=f1, f2=f2)
+
+
+# --------------------------------------------------------------------------
+# D1-D4 decoder and PCK cases
+# --------------------------------------------------------------------------
+def decode_cases():
+    return {
+        "valid64": dict(B=4, K=16, R=64, seed=201, centre="valid"),
+        "offc64": dict(B=3, K=9, R=64, seed=202, centre="off"),
+        "r96": dict(B=2, K=8, R=96, seed=203, centre="valid384"),
+    }
+
+
+def decode_inputs(B, K, R, seed, centre):
+    g = _g(seed)
+    hm = torch.randn(B, K, R, R, generator=g) * 0.1
+    # planted maxima
+    for b in range(B):
+        for k in range(K):
+            i = int(torch.randint(0, R * R, (1,), generator=g))
+            hm[b, k].view(-1)[i] = 1.0 + 0.01 * k
+    # exact ties: first index wins (utils/udaap/evaluation.py:18)
+    hm[0, 1].view(-1)[100] = 5.0
+    hm[0, 1].view(-1)[50] = 5.0
+    hm[0, 1].view(-1)[4000 % (R * R)] = 5.0
+    # all non-positive map -> zeroed prediction (evaluation.py:27-29)
+    hm[0, 2] = -torch.rand(R, R, generator=g) - 0.1
+    # all-zero map: max == 0 is not > 0
+    hm[1, 3] = 0.0
+    # corner maxima
+    hm[1, 0].view(-1)[0] = 9.0
+    hm[1, 1].view(-1)[R * R - 1] = 9.0
+    if centre == "valid":
+        center = torch.tensor([[128, 128]] * B, dtype=torch.int64)
+        scale = torch.tensor([256 / 200.0] * B, dtype=torch.float32)
+    elif centre == "valid384":
+        center = torch.tensor([[192, 192]] * B, dtype=torch.int64)
+        scale = torch.tensor([384 / 200.0] * B, dtype=torch.float32)
+    else:
+        center = torch.tensor([[128, 128], [100, 140], [131, 97]], dtype=torch.int64)[:B]
+        scale = torch.tensor([1.28, 1.1, 1.5], dtype=torch.float32)[:B]
+    return hm, center, scale
+
+
+def pck_cases():
+    return {
+        "mouse": dict(B=6, K=9, ref=[1, 2], thr=0.2, seed=301),
+        "lsp": dict(B=5, K=14, ref=[12, 13], thr=0.5, seed=302),
+        "flic": dict(B=4, K=11, ref=[3, 7], thr=0.5, seed=303),
+    }
+
+
+def pck_inputs(B, K, ref, thr, seed):
+    g = _g(seed)
+    gts = torch.zeros(B, K, 3)
+    gts[:, :, :2] = torch.randint(0, 256, (B, K, 2), generator=g).float()
+    gts[:, :, 2] = 1.0
+    preds = (gts[:, :, :2] + torch.randint(-30, 31, (B, K, 2), generator=g).float()).clone()
+    # invalid ground truths (x<=1 or y<=1) -> -1 sentinels (utils/evaluation.py:125-131)
+    gts[0, 0, 0] = 1.0
+    gts[1, 0, 1] = 0.0
+    gts[:, K - 1, 0] = 0.0          # a keypoint with no valid sample -> acc -1
+    preds[2, 3] = torch.tensor([-3.0, -3.0])   # a zeroed decoded point
+    return preds, gts
+
+
+# --------------------------------------------------------------------------
+# E1 EMA / S1 sampler
+# --------------------------------------------------------------------------
+def ema_inputs():
+    g = _g(401)
+    shapes = [(64, 3, 7, 7), (64,), (128, 64, 1, 1), (17,), (1,)]
+    ema = [torch.randn(*s, generator=g) for s in shapes]
+    cur = [torch.randn(*s, generator=g) for s in shapes]
+    return ema, cur
+
+
+def sampler_cases():
+    return {
+        "mouse": (list(range(30, 100)), list(range(30)), 4, 2, 1388),
+        "b32": (list(range(100, 500)), list(range(100)), 32, 16, 7),
+        "odd": ([5, 9, 2, 7, 11, 3, 8], [1, 4, 6], 5, 2, 3),
+    }
+
+
+# --------------------------------------------------------------------------
+# H1 hourglass cases
+# --------------------------------------------------------------------------
+def hg_cases():
+    return {
+        "hg2": dict(K=16, S=2, mode="AvgPool", seed=1388, B=2, res=256, sub=4, iseed=501),
+        "hg1k17": dict(K=17, S=1, mode="default", seed=7, B=1, res=128, sub=2, iseed=502),
+        "hg4max": dict(K=17, S=4, mode="MaxPool", seed=9, B=1, res=128, sub=2, iseed=503),
+    }
+
+
+def hg_inputs(K, S, mode, seed, B, res, sub, iseed):
+    g = _g(iseed)
+    x = torch.rand(B, 3, res, res, generator=g) - 0.45
+    R = res // 4
+    gp = torch.randn(B, S, K, R, R, generator=g)
+    gf = torch.randn(B, S, 256, R // 2, R // 2, generator=g)
+    return x, gp, gf
+
+
+# --------------------------------------------------------------------------
+# T1 one training step per project
+# --------------------------------------------------------------------------
+MEANS = [0.4920829, 0.4920829, 0.4920829]
+
+
+def step_cases():
+    base = dict(res=256, out=64, poseWeight=10.0, ensemblePseudoWeight=10.0, FDLWeight=1.0,
+                pseudoWeight=1.0, ema_decay=0.999, lr=2.5e-4, FDL_label="labeled",
+                FDL_type="covariance")
+    return {
+        "mt_ubpl": dict(base, project="MT_UBPL", S=2, K=16, B=4, nlab=2, epo=1, consWeight=3.0,
+                        thr=0.15, mode="AvgPool", brNum=2, A=2, seed=601),
+        "mt_ubpl_e0": dict(base, project="MT_UBPL", S=2, K=16, B=4, nlab=2, epo=0, consWeight=0.0,
+                           thr=0.95, mode="AvgPool", brNum=2, A=2, seed=602, FDLWeight=0.5),
+        "dualpose": dict(base, project="DualPose_UBPL", S=2, K=17, B=4, nlab=2, epo=2, consWeight=5.0,
+                         thr=0.15, mode="AvgPool", brNum=2, A=1, seed=603, pseudoWeight=0.5),
+        "mt": dict(base, project="MT", S=2, K=16, B=4, nlab=2, epo=1, consWeight=2.0, thr=0.95,
+                   mode="AvgPool", brNum=1, A=2, seed=604),
+        "sup": dict(base, project="supervised", S=1, K=16, B=4, nlab=4, epo=0, consWeight=0.0,
+                    thr=0.95, mode="default", brNum=1, A=1, seed=605),
+    }
+
+
+def step_models(factory, cfg, device="cpu"):
+    """Models built in the reference's order (projects/MT_UBPL.py:43-50): per
+    branch a student, then an independently initialised teacher."""
+    torch.manual_seed(1388)
+    models, emas, optims = [], [], []
+    for _ in range(cfg["brNum"]):
+        m = factory(cfg["K"], cfg["S"], cfg["mode"])
+        models.append(m)
+        if cfg["project"] != "supervised":
+            e = factory(cfg["K"], cfg["S"], cfg["mode"])
+            for p in e.parameters():
+                p.detach_()
+            emas.append(e)
+    models = [m.to(device) for m in models]
+    emas = [e.to(device) for e in emas]
+    for m in models:
+        optims.append(torch.optim.AdamW(m.parameters(), lr=cfg["lr"], weight_decay=0))
+    return models, emas, optims
+
+
+def step_raw(cfg):
+    """Images and keypoints for one batch (unlabeled rows first, as
+    TwoStreamBatchSampler orders them: utils/mt/data.py:105-132)."""
+    g = _g(cfg["seed"])
+    B, K, A, res = cfg["B"], cfg["K"], cfg["A"], cfg["res"]
+    nviews = A if cfg["project"] != "DualPose_UBPL" else 2
+    means = torch.tensor(MEANS)[None, :, None, None]
+    imgs = [torch.rand(B, 3, res, res, generator=g) - means for _ in range(nviews)]
+    isl = torch.tensor([0] * (B - cfg["nlab"]) + [1] * cfg["nlab"], dtype=torch.bool)
+    kps = []
+    for _ in range(nviews):
+        k = torch.zeros(B, K, 3)
+        k[:, :, :2] = torch.randint(8, res - 8, (B, K, 2), generator=g).float()
+        k[:, :, 2] = 1.0
+        k[~isl] = 0.0
+        kps.append(k)
+    return imgs, kps, isl
+
+
+def step_batch(cfg, render):
+    """Build the (loader, args) pair the reference train() consumes.  `render`
+    has the signature of ProcessUtils.kps_heatmap (utils/process.py:253)."""
+    imgs, kps, isl = step_raw(cfg)
+    res, out = cfg["res"], cfg["out"]
+    hms, gates = [], []
+    for k in kps:
+        hb, gb = [], []
+        for b in range(k.shape[0]):
+            hm, kk = render(k[b].clone(), (3, res, res), res, out)
+            hb.append(hm)
+            gb.append(kk[:, 2].clone())
+        hms.append(torch.stack(hb))
+        gates.append(torch.stack(gb))
+    B = cfg["B"]
+    if cfg["project"] == "DualPose_UBPL":
+        meta = {"kpsWeight": gates[0], "islabeled": isl}
+        batch = (imgs[0], hms[0], imgs[1], meta)
+    elif cfg["project"] == "supervised":
+        batch = (imgs[0], hms[0], {"islabeled": isl})
+    else:
+        A = cfg["A"]
+        meta = {"kpsWeights": [[gates[a]] for a in range(A)],
+                "warpmat": [torch.zeros(B, 2, 3) for _ in range(A)],
+                "isflip": [torch.zeros(B, dtype=torch.bool) for _ in range(A)],
+                "islabeled": [isl]}
+        batch = (imgs, [[hms[a]] for a in range(A)], meta)
+    args = types.SimpleNamespace(
+        device="cpu", debug=False, br_augNum=1, br_gtNum=1, nStack=cfg["S"], useEnsemblePseudo=True,
+        pseudoScoreThr=cfg["thr"], ensemblePseudoWeight=cfg["ensemblePseudoWeight"],
+        consWeight=cfg["consWeight"], poseWeight=cfg["poseWeight"], FDLWeight=cfg["FDLWeight"],
+        FDL_label=cfg["FDL_label"], FDL_type=cfg["FDL_type"], epo=cfg["epo"], ema_decay=cfg["ema_decay"],
+        pseudoWeight=cfg["pseudoWeight"], lr=cfg["lr"], feature_mode=cfg["mode"])
+    return [batch], args
+
+
+def bn_cancelled(name):
+    """Conv biases whose exact gradient is zero.  A per-channel constant added by
+    any conv bias reaches the outputs only through identity skips, max-pool,
+    nearest-upsample, 1x1 skip/merge convs and additions, all of which carry a
+    per-channel constant forward unchanged (or linearly), until a train-mode
+    BatchNorm subtracts it (models/base/layers.py:45-47,74-84,104-111;
+    models/pose/hourglass.py:66-83).  Only the `preds` heads escape this.  The
+    gradient any implementation computes for the others is rounding noise of
+    large cancelling sums, so AdamW's first step on them (lr * g/(|g|+eps)) has
+    a noise-determined sign in the reference as well."""
+    return name.endswith("conv.bias") and not name.startswith("preds.")
