@@ -1,0 +1,130 @@
+/*
+ * ubpl_hip.h — C-ABI of libubpl_hip.so, the MI355X (gfx950) hot path of
+ * Qi2019KB/UBPL-PoseEstimation's semi-supervised pose training step.
+ *
+ * Conventions
+ *   - plain pointers to DEVICE memory, sizes as int / int64_t, no torch types;
+ *   - every function enqueues on `stream` (a hipStream_t, NULL = default
+ *     stream), never synchronises, never allocates: scratch is caller-owned;
+ *   - return 0 on success, otherwise a hipError_t code (e.g. 1 =
+ *     hipErrorInvalidValue for an unsupported shape);
+ *   - layouts are the reference's: NCHW float32 tensors, contiguous.
+ *
+ * Reference interfaces replaced (paths relative to the reference root) are
+ * cited per entry.  The Python host layer (ubpl-poseestimation_amd/ubpl_amd)
+ * binds these through ctypes and re-exposes the reference's module API.
+ */
+#ifndef UBPL_HIP_H
+#define UBPL_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- R1 ----
+ * ProcessUtils.kps_heatmap / kps_heatmap_mulKps (utils/process.py:252-318).
+ * kps [N,K,3] (x, y, vis) in image pixels -> hm [N,K,size_h,size_w] with
+ * size = int(img / (inp_res/out_res)); kps_out[...,2] = vis * visible
+ * (may alias kps: the reference mutates kpsMap in place, :267). */
+int ubpl_render_heatmaps(const float* kps, float* hm, float* kps_out, int N, int K, int img_h, int img_w,
+                         int inp_res, int out_res, float kernel_size, float sigma, float cutoff, void* stream);
+
+/* ---------------------------------------------------------------- L1-L4 --
+ * Row statistics of mean_px((a - t)^2): a row (b,s,k) at a + b*a_sb + s*a_ss + k*HW;
+ * target = mean over m < M of t + m*t_sm + b*t_sb + s*t_ss + k*HW.
+ * Outputs [B*S*K]: sq_mean; amax = max_px a (nullable); tmax = max_px target (nullable).
+ * JointMSELoss / JointDistLoss / JointDistLoss_mt2 / JointPseudoLoss3 forward
+ * (utils/losses.py:16-53, 255-286, 176-210). */
+int ubpl_heatmap_row_stats(const float* a, int64_t a_sb, int64_t a_ss, const float* t, int64_t t_sb, int64_t t_ss,
+                           int64_t t_sm, int M, int B, int S, int K, int HW, float* sq_mean, float* amax,
+                           float* tmax, void* stream);
+/* Loss reduction + counts on device.  kind 0 MSE/consistency, 1 teacher-
+ * confidence mask (mt2), 2 UBPL pseudo mask.  out_sum[1] f32; out_cnt[4] int32 =
+ * {nStack*#gate>0, n_pseudo, n_sel, #rows sw>0}; out_score[K] (kinds 1,2);
+ * out_w[B*S*K] per-row weight for the backward. */
+int ubpl_loss_finalize(int kind, const float* sq_mean, const float* amax, const float* tmax, const float* gate,
+                       const float* sw, int use_gate, int use_sw, int B, int S, int K, float thr, float* out_sum,
+                       int* out_cnt, float* out_score, float* out_w, void* stream);
+/* d a (+)= w_row * (*gscale) * extra * (a - target); gscale device scalar (nullable = 1). */
+int ubpl_heatmap_row_grad(const float* a, int64_t a_sb, int64_t a_ss, const float* t, int64_t t_sb, int64_t t_ss,
+                          int64_t t_sm, int M, int B, int S, int K, int HW, const float* w, const float* gscale,
+                          float extra, float* da, int accumulate, void* stream);
+
+/* ---------------------------------------------------------------- L5 ----
+ * ProcessUtils.features_cov (utils/process.py:18-31) over rows whose
+ * rowmask[b] > 0 (the caller's labeled-row selection, projects/MT_UBPL.py:309-320).
+ * f1,f2 [B,S,C,HW]; cov/mu1/mu2 [B*S*C] scratch; out_val[1] = mean |cov|;
+ * out_cnt[1] = #selected * S * C. */
+int ubpl_fdl_cov_forward(const float* f1, const float* f2, const float* rowmask, int B, int S, int C, int HW,
+                         float* cov, float* mu1, float* mu2, float* out_val, int* out_cnt, void* stream);
+int ubpl_fdl_cov_backward(const float* f1, const float* f2, const float* rowmask, const float* cov, const float* mu1,
+                          const float* mu2, const int* cnt, const float* gscale, int B, int S, int C, int HW,
+                          float* d1, float* d2, int accumulate, void* stream);
+
+/* ---------------------------------------------------------------- D1-D4 --
+ * get_preds + final_preds + kps_fromHeatmap (utils/udaap/evaluation.py:13-30,215-238;
+ * utils/process.py:320-327).  tinv [N,6] f64 = rows 0-1 of inv(get_transform)
+ * (nullable: no transform).  raw/preds [N,K,2], scores [N,K] (each nullable). */
+int ubpl_decode_heatmaps(const float* hm, int N, int K, int H, int W, const double* tinv, float* raw, float* preds,
+                         float* scores, void* stream);
+/* EvaluationUtils.acc_pck (utils/evaluation.py:91-139).  errs/accs [K+1];
+ * hits/valid [K] int32 (nullable) for cross-rank aggregation. */
+int ubpl_pck(const float* preds, const float* gts, int N, int K, int ref0, int ref1, float thr, float* errs,
+             float* accs, int* hits, int* valid, void* stream);
+
+/* ---------------------------------------------------------------- E1 ----
+ * update_ema_variables (utils/parameters.py:4-8) on a flat parameter buffer. */
+int ubpl_ema_update(float* ema, const float* p, int64_t n, double alpha, void* stream);
+/* torch.optim.AdamW step (the optimizer projects/MT_UBPL.py:48 builds) on flat buffers. */
+int ubpl_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
+                    double eps, double weight_decay, int64_t step, void* stream);
+int ubpl_scale_(float* x, int64_t n, float s, void* stream);
+
+/* ---------------------------------------------------------------- H2-H4 --
+ * BatchNorm2d (models/base/layers.py:41,57-61), train-mode statistics.
+ * part: scratch of 2*C*ubpl_bn_splits(B,C) doubles.  rmean/rvar updated with
+ * momentum (nullable).  scale = gamma*invstd, shift = beta - mean*scale. */
+int ubpl_bn_splits(int B, int C);
+int ubpl_bn_forward_stats(const float* x, int B, int C, int HW, const float* gamma, const float* beta, float eps,
+                          float momentum, float* rmean, float* rvar, double* part, float* mean_out,
+                          float* invstd_out, float* scale, float* shift, void* stream);
+int ubpl_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
+                        int C, float* scale, float* shift, void* stream);
+int ubpl_bn_apply(const float* x, int B, int C, int HW, const float* scale, const float* shift, int relu, float* y,
+                  void* stream);
+/* Backward of y = [relu](bn(x)); dgamma/dbeta accumulate; dx = add1 + add2 + dL/dx. */
+int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma, const float* mean,
+                     const float* invstd, const float* scale, const float* shift, int relu, double* part,
+                     float* coef, float* dgamma, float* dbeta, const float* add1, const float* add2, float* dx,
+                     void* stream);
+
+/* Conv (models/base/layers.py:31-50): 1x1/s1, 3x3/s1, 7x7/s2, pad (KS-1)/2,
+ * optional fused pre-activation relu(x*pscale + pshift), bias, residual add
+ * (res may alias y).  MFMA f32 implicit GEMM. */
+int ubpl_conv2d_forward(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias, int Cout,
+                        int KS, int stride, const float* pscale, const float* pshift, const float* res, float* y,
+                        int Ho, int Wo, void* stream);
+int64_t ubpl_conv2d_wgrad_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo);
+int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, int H, int W, int Cout, int KS, int stride,
+                      const float* pscale, const float* pshift, int Ho, int Wo, float* slab, float* dw, float* db,
+                      int accumulate, void* stream);
+int ubpl_conv_weight_flip(const float* w, int Cout, int Cin, int KS, float* wt, void* stream);
+
+/* MaxPool2d(2,2) (models/base/layers.py:93), Upsample(x2, nearest) + add
+ * (layers.py:110-111), AvgPool2d(2,2) projection (models/pose/hourglass.py:226). */
+int ubpl_maxpool2x2_forward(const float* x, int64_t planes, int H, int W, float* y, void* stream);
+int ubpl_maxpool2x2_backward(const float* x, const float* dy, int64_t planes, int H, int W, float* dx,
+                             int accumulate, void* stream);
+int ubpl_avgpool2x2_forward(const float* x, int64_t planes, int H, int W, float* y, void* stream);
+int ubpl_avgpool2x2_backward(const float* dy, int64_t planes, int H, int W, float* dx, int accumulate, void* stream);
+int ubpl_upsample2x_add_forward(const float* up, const float* low, int64_t planes, int H, int W, float* out,
+                                void* stream);
+int ubpl_upsample2x_add_backward(const float* dout, int64_t planes, int H, int W, float* dlow, int accumulate,
+                                 void* stream);
+int ubpl_add(const float* a, const float* b, int64_t n, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UBPL_HIP_H */

@@ -1,0 +1,278 @@
+// BatchNorm2d (train-mode batch statistics, eval-mode running statistics) for
+// the hourglass (models/base/layers.py:41,57-61; nn.BatchNorm2d momentum 0.1,
+// eps 1e-5).  NCHW: a channel is B contiguous HW planes.
+//
+// Forward never materialises bn(x) for the residual branches: the statistics
+// kernels produce per-channel (scale, shift) = (g*invstd, b - mean*g*invstd)
+// — PyTorch's own transform form — and the consuming convolution applies
+// relu(x*scale + shift) while staging its operand (conv.hip prologue).
+//
+// Statistics: each (channel, batch-slice) workgroup accumulates sum and sum of
+// squares of (x - x0) — x0 a sample of the channel, which removes the
+// cancellation of E[x^2] - E[x]^2 — then reduces in f64.  Partials are written
+// to a slab and combined by a finalize kernel: deterministic, no atomics.
+//
+// Backward: dyp = dz * [x*scale + shift > 0] (ReLU mask recomputed bit-for-bit
+// as the forward prologue computed it); per channel S1 = sum dyp,
+// S2 = sum dyp*(x - mean); dbeta += S1, dgamma += S2*invstd;
+// dx = a*dyp + b*(x - mean) + c with a = g*invstd, b = -g*invstd^3*S2/N,
+// c = -g*invstd*S1/N, plus up to two addends (residual-gradient sums).
+#include "common.h"
+
+namespace {
+
+template <bool VEC>
+__global__ void __launch_bounds__(256) stats_partial_kernel(const float* __restrict__ x, int B, int C, int HW,
+                                                           int bper, double* __restrict__ part) {
+    __shared__ double red[16];
+    const int c = blockIdx.x, sp = blockIdx.y;
+    const int b0 = sp * bper, b1 = min(B, b0 + bper);
+    const float x0 = x[(int64_t)c * HW];
+    float s1 = 0.f, s2 = 0.f;
+    for (int b = b0; b < b1; ++b) {
+        const float* p = x + ((int64_t)b * C + c) * HW;
+        if (VEC) {
+            const float4* p4 = reinterpret_cast<const float4*>(p);
+            for (int i = threadIdx.x; i < (HW >> 2); i += blockDim.x) {
+                const float4 v = p4[i];
+                const float a = v.x - x0, bb = v.y - x0, cc = v.z - x0, d = v.w - x0;
+                s1 += (a + bb) + (cc + d);
+                s2 = fmaf(a, a, fmaf(bb, bb, fmaf(cc, cc, fmaf(d, d, s2))));
+            }
+        } else {
+            for (int i = threadIdx.x; i < HW; i += blockDim.x) {
+                const float a = p[i] - x0;
+                s1 += a;
+                s2 = fmaf(a, a, s2);
+            }
+        }
+    }
+    const double d1 = ubpl::block_sum((double)s1, red);
+    const double d2 = ubpl::block_sum((double)s2, red);
+    if (threadIdx.x == 0) {
+        part[((int64_t)c * gridDim.y + sp) * 2 + 0] = d1;
+        part[((int64_t)c * gridDim.y + sp) * 2 + 1] = d2;
+    }
+}
+
+__global__ void stats_finalize_kernel(const float* __restrict__ x, const double* __restrict__ part, int C, int HW,
+                                      int splits, int64_t N, const float* __restrict__ gamma,
+                                      const float* __restrict__ beta, float eps, float momentum,
+                                      float* __restrict__ rmean, float* __restrict__ rvar,
+                                      float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                      float* __restrict__ scale, float* __restrict__ shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s1 = 0.0, s2 = 0.0;
+    for (int s = 0; s < splits; ++s) {
+        s1 += part[((int64_t)c * splits + s) * 2 + 0];
+        s2 += part[((int64_t)c * splits + s) * 2 + 1];
+    }
+    const double x0 = (double)x[(int64_t)c * HW];
+    const double m1 = s1 / (double)N;
+    double var = s2 / (double)N - m1 * m1;
+    if (var < 0) var = 0;
+    const double mean = x0 + m1;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma[c];
+    const float sc = invstd * g;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = invstd;
+    scale[c] = sc;
+    shift[c] = beta[c] - (float)mean * sc;
+    if (rmean) {
+        const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
+        rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
+        rvar[c] = (float)((double)momentum * unb + (1.0 - (double)momentum) * (double)rvar[c]);
+    }
+}
+
+__global__ void eval_coeff_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                  const float* __restrict__ rmean, const float* __restrict__ rvar, float eps, int C,
+                                  float* __restrict__ scale, float* __restrict__ shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float invstd = (float)(1.0 / sqrt((double)rvar[c] + (double)eps));
+    const float sc = invstd * gamma[c];
+    scale[c] = sc;
+    shift[c] = beta[c] - rmean[c] * sc;
+}
+
+__global__ void __launch_bounds__(256) apply_kernel(const float* __restrict__ x, const float* __restrict__ scale,
+                                                   const float* __restrict__ shift, int C, int HW, int64_t total4,
+                                                   int relu, float* __restrict__ y) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int hw4 = HW >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += stride) {
+        const int c = (int)((i / hw4) % C);
+        const float sc = scale[c], sh = shift[c];
+        float4 v = reinterpret_cast<const float4*>(x)[i];
+        v.x = fmaf(v.x, sc, sh);
+        v.y = fmaf(v.y, sc, sh);
+        v.z = fmaf(v.z, sc, sh);
+        v.w = fmaf(v.w, sc, sh);
+        if (relu) {
+            v.x = fmaxf(v.x, 0.f);
+            v.y = fmaxf(v.y, 0.f);
+            v.z = fmaxf(v.z, 0.f);
+            v.w = fmaxf(v.w, 0.f);
+        }
+        reinterpret_cast<float4*>(y)[i] = v;
+    }
+}
+
+__global__ void __launch_bounds__(256) bwd_partial_kernel(const float* __restrict__ dz, const float* __restrict__ x,
+                                                         int B, int C, int HW, int bper,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift,
+                                                         const float* __restrict__ mean, int relu,
+                                                         double* __restrict__ part) {
+    __shared__ double red[16];
+    const int c = blockIdx.x, sp = blockIdx.y;
+    const int b0 = sp * bper, b1 = min(B, b0 + bper);
+    const float sc = scale[c], sh = shift[c], mu = mean[c];
+    float s1 = 0.f, s2 = 0.f;
+    for (int b = b0; b < b1; ++b) {
+        const int64_t off = ((int64_t)b * C + c) * HW;
+        for (int i = threadIdx.x; i < HW; i += blockDim.x) {
+            const float xv = x[off + i];
+            float g = dz[off + i];
+            if (relu && !(fmaf(xv, sc, sh) > 0.f)) g = 0.f;
+            s1 += g;
+            s2 = fmaf(g, xv - mu, s2);
+        }
+    }
+    const double d1 = ubpl::block_sum((double)s1, red);
+    const double d2 = ubpl::block_sum((double)s2, red);
+    if (threadIdx.x == 0) {
+        part[((int64_t)c * gridDim.y + sp) * 2 + 0] = d1;
+        part[((int64_t)c * gridDim.y + sp) * 2 + 1] = d2;
+    }
+}
+
+__global__ void bwd_finalize_kernel(const double* __restrict__ part, int C, int splits, int64_t N,
+                                    const float* __restrict__ gamma, const float* __restrict__ invstd,
+                                    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ ca,
+                                    float* __restrict__ cb, float* __restrict__ cc) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s1 = 0.0, s2 = 0.0;
+    for (int s = 0; s < splits; ++s) {
+        s1 += part[((int64_t)c * splits + s) * 2 + 0];
+        s2 += part[((int64_t)c * splits + s) * 2 + 1];
+    }
+    const double is = invstd[c], g = gamma[c];
+    if (dgamma) dgamma[c] += (float)(s2 * is);
+    if (dbeta) dbeta[c] += (float)s1;
+    ca[c] = (float)(g * is);
+    cb[c] = (float)(-g * is * is * is * s2 / (double)N);
+    cc[c] = (float)(-g * is * s1 / (double)N);
+}
+
+__global__ void __launch_bounds__(256) bwd_apply_kernel(const float* __restrict__ dz, const float* __restrict__ x,
+                                                       int C, int HW, int64_t total,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float* __restrict__ mean, int relu,
+                                                       const float* __restrict__ ca, const float* __restrict__ cb,
+                                                       const float* __restrict__ cc, const float* add1,
+                                                       const float* add2, float* dx) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int c = (int)((i / HW) % C);
+        const float xv = x[i];
+        float g = dz[i];
+        if (relu && !(fmaf(xv, scale[c], shift[c]) > 0.f)) g = 0.f;
+        float v = fmaf(ca[c], g, fmaf(cb[c], xv - mean[c], cc[c]));
+        if (add1) v += add1[i];
+        if (add2) v += add2[i];
+        dx[i] = v;
+    }
+}
+
+int splits_for(int B, int C) {
+    int s = (2048 + C - 1) / C;
+    if (s > B) s = B;
+    if (s < 1) s = 1;
+    return s;
+}
+
+int grid_ew(int64_t n) {
+    int64_t g = (n + 255) / 256;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace
+
+// Scratch: part must hold C * ubpl_bn_splits(B, C) * 2 doubles.
+UBPL_API int ubpl_bn_splits(int B, int C) { return splits_for(B, C); }
+
+// Train-mode statistics of x [B,C,H,W] -> mean, invstd, (scale, shift) and the
+// running-stat update (rmean/rvar nullable: track_running_stats off).
+UBPL_API int ubpl_bn_forward_stats(const float* x, int B, int C, int HW, const float* gamma, const float* beta,
+                                   float eps, float momentum, float* rmean, float* rvar, double* part,
+                                   float* mean_out, float* invstd_out, float* scale, float* shift, void* stream) {
+    const int splits = splits_for(B, C);
+    const int bper = (B + splits - 1) / splits;
+    const int gs = (B + bper - 1) / bper;
+    const bool vec = (HW % 4 == 0) && (((uintptr_t)x & 15) == 0);
+    if (vec)
+        hipLaunchKernelGGL(stats_partial_kernel<true>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, x, B, C, HW,
+                           bper, part);
+    else
+        hipLaunchKernelGGL(stats_partial_kernel<false>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, x, B, C, HW,
+                           bper, part);
+    UBPL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(stats_finalize_kernel, dim3(ubpl::cdiv(C, 64)), dim3(64), 0, (hipStream_t)stream, x, part, C,
+                       HW, gs, (int64_t)B * HW, gamma, beta, eps, momentum, rmean, rvar, mean_out, invstd_out, scale,
+                       shift);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+UBPL_API int ubpl_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                                 float eps, int C, float* scale, float* shift, void* stream) {
+    hipLaunchKernelGGL(eval_coeff_kernel, dim3(ubpl::cdiv(C, 64)), dim3(64), 0, (hipStream_t)stream, gamma, beta,
+                       rmean, rvar, eps, C, scale, shift);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// y = [relu](x*scale + shift); HW must be a multiple of 4, x/y 16-B aligned.
+UBPL_API int ubpl_bn_apply(const float* x, int B, int C, int HW, const float* scale, const float* shift, int relu,
+                           float* y, void* stream) {
+    if ((HW & 3) || (((uintptr_t)x | (uintptr_t)y) & 15)) return (int)hipErrorInvalidValue;
+    const int64_t total4 = (int64_t)B * C * HW / 4;
+    hipLaunchKernelGGL(apply_kernel, dim3(grid_ew(total4)), dim3(256), 0, (hipStream_t)stream, x, scale, shift, C, HW,
+                       total4, relu, y);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// Backward of y = [relu](bn(x)) given dz = dL/dy.  dgamma/dbeta are
+// ACCUMULATED (+=).  dx = add1 + add2 + dL/dx (add1/add2 nullable; dx may
+// alias dz, add1 or add2).  coef: scratch of 3*C floats.
+UBPL_API int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma,
+                              const float* mean, const float* invstd, const float* scale, const float* shift,
+                              int relu, double* part, float* coef, float* dgamma, float* dbeta, const float* add1,
+                              const float* add2, float* dx, void* stream) {
+    const int splits = splits_for(B, C);
+    const int bper = (B + splits - 1) / splits;
+    const int gs = (B + bper - 1) / bper;
+    hipLaunchKernelGGL(bwd_partial_kernel, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW, bper,
+                       scale, shift, mean, relu, part);
+    UBPL_LAUNCH_CHECK();
+    float* ca = coef;
+    float* cb = coef + C;
+    float* cc = coef + 2 * C;
+    hipLaunchKernelGGL(bwd_finalize_kernel, dim3(ubpl::cdiv(C, 64)), dim3(64), 0, (hipStream_t)stream, part, C, gs,
+                       (int64_t)B * HW, gamma, invstd, dgamma, dbeta, ca, cb, cc);
+    UBPL_LAUNCH_CHECK();
+    const int64_t total = (int64_t)B * C * HW;
+    hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_ew(total)), dim3(256), 0, (hipStream_t)stream, dz, x, C, HW, total,
+                       scale, shift, mean, relu, ca, cb, cc, add1, add2, dx);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}

@@ -1,0 +1,212 @@
+// Hourglass resampling: MaxPool2d(2,2) (models/base/layers.py:93, hourglass.py:24),
+// nearest Upsample(x2) + skip add (layers.py:102,110-111), and the feature
+// projection AvgPool2d(2,2) (models/pose/hourglass.py:92-99).  All HBM-bound;
+// one thread per output pair (float2 along W), backward recomputes the
+// max-pool argmax from the saved input (first maximum in row-major window
+// order, as PyTorch's CPU kernel) instead of storing indices.
+#include "common.h"
+
+namespace {
+
+int grid_ew(int64_t n) {
+    int64_t g = (n + 255) / 256;
+    if (g > 8192) g = 8192;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+// planes = B*C; output Ho x Wo with Ho = H/2, Wo = W/2 (floor).
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const float* __restrict__ x, int64_t planes, int H, int W,
+                                                         float* __restrict__ y) {
+    const int Ho = H >> 1, Wo = W >> 1;
+    const int64_t total = planes * Ho * Wo;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int ow = (int)(i % Wo);
+        const int64_t t = i / Wo;
+        const int oh = (int)(t % Ho);
+        const int64_t pl = t / Ho;
+        const float* p = x + (pl * H + 2 * oh) * W + 2 * ow;
+        float m = p[0];
+        float v = p[1];
+        if (v > m || isnan(v)) m = v;
+        v = p[W];
+        if (v > m || isnan(v)) m = v;
+        v = p[W + 1];
+        if (v > m || isnan(v)) m = v;
+        y[i] = m;
+    }
+}
+
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                         int64_t planes, int H, int W, float* __restrict__ dx,
+                                                         int accumulate) {
+    const int Ho = H >> 1, Wo = W >> 1;
+    const int64_t total = planes * Ho * Wo;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int ow = (int)(i % Wo);
+        const int64_t t = i / Wo;
+        const int oh = (int)(t % Ho);
+        const int64_t pl = t / Ho;
+        const int64_t base = (pl * H + 2 * oh) * W + 2 * ow;
+        const float* p = x + base;
+        int am = 0;
+        float m = p[0];
+        const int offs[4] = {0, 1, W, W + 1};
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+            const float v = p[offs[q]];
+            if (v > m || isnan(v)) {
+                m = v;
+                am = q;
+            }
+        }
+        const float g = dy[i];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float v = (q == am) ? g : 0.f;
+            float* d = dx + base + offs[q];
+            *d = accumulate ? *d + v : v;
+        }
+    }
+}
+
+// y = (sum of the 2x2 window) / 4, summed row-major like avg_pool2d's CPU loop.
+__global__ void __launch_bounds__(256) avgpool_fwd_kernel(const float* __restrict__ x, int64_t planes, int H, int W,
+                                                         float* __restrict__ y) {
+    const int Ho = H >> 1, Wo = W >> 1;
+    const int64_t total = planes * Ho * Wo;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int ow = (int)(i % Wo);
+        const int64_t t = i / Wo;
+        const int oh = (int)(t % Ho);
+        const int64_t pl = t / Ho;
+        const float* p = x + (pl * H + 2 * oh) * W + 2 * ow;
+        y[i] = (((p[0] + p[1]) + p[W]) + p[W + 1]) / 4.f;
+    }
+}
+
+__global__ void __launch_bounds__(256) avgpool_bwd_kernel(const float* __restrict__ dy, int64_t planes, int H, int W,
+                                                         float* __restrict__ dx, int accumulate) {
+    const int Ho = H >> 1, Wo = W >> 1;
+    const int64_t total = planes * Ho * Wo;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int ow = (int)(i % Wo);
+        const int64_t t = i / Wo;
+        const int oh = (int)(t % Ho);
+        const int64_t pl = t / Ho;
+        const int64_t base = (pl * H + 2 * oh) * W + 2 * ow;
+        const float g = dy[i] / 4.f;
+        const int64_t offs[4] = {0, 1, W, W + 1};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float* d = dx + base + offs[q];
+            *d = accumulate ? *d + g : g;
+        }
+    }
+}
+
+// out[b,c,h,w] = up[b,c,h,w] + low[b,c,h/2,w/2]   (out may alias up)
+__global__ void __launch_bounds__(256) upadd_fwd_kernel(const float* up, const float* __restrict__ low,
+                                                       int64_t planes, int H, int W, float* out) {
+    const int Hl = H >> 1, Wl = W >> 1;
+    const int64_t total = planes * H * W;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int w = (int)(i % W);
+        const int64_t t = i / W;
+        const int h = (int)(t % H);
+        const int64_t pl = t / H;
+        out[i] = up[i] + low[(pl * Hl + (h >> 1)) * Wl + (w >> 1)];
+    }
+}
+
+// dlow[b,c,i,j] (+)= sum of the 2x2 block of dout (upsample_nearest2d backward)
+__global__ void __launch_bounds__(256) upadd_bwd_kernel(const float* __restrict__ dout, int64_t planes, int H, int W,
+                                                       float* __restrict__ dlow, int accumulate) {
+    const int Hl = H >> 1, Wl = W >> 1;
+    const int64_t total = planes * Hl * Wl;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int j = (int)(i % Wl);
+        const int64_t t = i / Wl;
+        const int r = (int)(t % Hl);
+        const int64_t pl = t / Hl;
+        const float* p = dout + (pl * H + 2 * r) * W + 2 * j;
+        const float s = ((p[0] + p[1]) + p[W]) + p[W + 1];
+        dlow[i] = accumulate ? dlow[i] + s : s;
+    }
+}
+
+__global__ void __launch_bounds__(256) add_kernel(const float* a, const float* b, int64_t n, float* out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = a[i] + b[i];
+}
+
+}  // namespace
+
+UBPL_API int ubpl_maxpool2x2_forward(const float* x, int64_t planes, int H, int W, float* y, void* stream) {
+    const int64_t n = planes * (H / 2) * (W / 2);
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, x, planes, H, W, y);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+UBPL_API int ubpl_maxpool2x2_backward(const float* x, const float* dy, int64_t planes, int H, int W, float* dx,
+                                      int accumulate, void* stream) {
+    const int64_t n = planes * (H / 2) * (W / 2);
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, x, dy, planes, H, W,
+                       dx, accumulate);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+UBPL_API int ubpl_avgpool2x2_forward(const float* x, int64_t planes, int H, int W, float* y, void* stream) {
+    const int64_t n = planes * (H / 2) * (W / 2);
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, x, planes, H, W, y);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+UBPL_API int ubpl_avgpool2x2_backward(const float* dy, int64_t planes, int H, int W, float* dx, int accumulate,
+                                      void* stream) {
+    const int64_t n = planes * (H / 2) * (W / 2);
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, dy, planes, H, W, dx,
+                       accumulate);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+UBPL_API int ubpl_upsample2x_add_forward(const float* up, const float* low, int64_t planes, int H, int W, float* out,
+                                         void* stream) {
+    const int64_t n = planes * H * W;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(upadd_fwd_kernel, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, up, low, planes, H, W,
+                       out);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+UBPL_API int ubpl_upsample2x_add_backward(const float* dout, int64_t planes, int H, int W, float* dlow,
+                                          int accumulate, void* stream) {
+    const int64_t n = planes * (H / 2) * (W / 2);
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(upadd_bwd_kernel, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, dout, planes, H, W, dlow,
+                       accumulate);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+UBPL_API int ubpl_add(const float* a, const float* b, int64_t n, float* out, void* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(add_kernel, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, a, b, n, out);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}

@@ -1,0 +1,93 @@
+"""ctypes binding of libubpl_hip.so (C-ABI declared in include/ubpl_hip.h).
+
+torch is imported first so that the library binds to the HIP runtime torch
+already loaded (same SONAME, one runtime, one set of streams).  There is no
+CPU fallback: a missing library or a missing GPU raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libubpl_hip.so")
+
+P, I, L, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double
+
+# name -> (restype, argtypes) — mirrors include/ubpl_hip.h
+SIGNATURES = {
+    "ubpl_render_heatmaps": (I, [P, P, P, I, I, I, I, I, I, F, F, F, P]),
+    "ubpl_heatmap_row_stats": (I, [P, L, L, P, L, L, L, I, I, I, I, I, P, P, P, P]),
+    "ubpl_loss_finalize": (I, [I, P, P, P, P, P, I, I, I, I, I, F, P, P, P, P, P]),
+    "ubpl_heatmap_row_grad": (I, [P, L, L, P, L, L, L, I, I, I, I, I, P, P, F, P, I, P]),
+    "ubpl_fdl_cov_forward": (I, [P, P, P, I, I, I, I, P, P, P, P, P, P]),
+    "ubpl_fdl_cov_backward": (I, [P, P, P, P, P, P, P, P, I, I, I, I, P, P, I, P]),
+    "ubpl_decode_heatmaps": (I, [P, I, I, I, I, P, P, P, P, P]),
+    "ubpl_pck": (I, [P, P, I, I, I, I, F, P, P, P, P, P]),
+    "ubpl_ema_update": (I, [P, P, L, D, P]),
+    "ubpl_adamw_step": (I, [P, P, P, P, L, D, D, D, D, D, L, P]),
+    "ubpl_scale_": (I, [P, L, F, P]),
+    "ubpl_bn_splits": (I, [I, I]),
+    "ubpl_bn_forward_stats": (I, [P, I, I, I, P, P, F, F, P, P, P, P, P, P, P, P]),
+    "ubpl_bn_eval_coeffs": (I, [P, P, P, P, F, I, P, P, P]),
+    "ubpl_bn_apply": (I, [P, I, I, I, P, P, I, P, P]),
+    "ubpl_bn_backward": (I, [P, P, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, P, P]),
+    "ubpl_conv2d_forward": (I, [P, I, I, I, I, P, P, I, I, I, P, P, P, P, I, I, P]),
+    "ubpl_conv2d_wgrad_workspace": (L, [I, I, I, I, I, I]),
+    "ubpl_conv2d_wgrad": (I, [P, P, I, I, I, I, I, I, I, P, P, I, I, P, P, P, I, P]),
+    "ubpl_conv_weight_flip": (I, [P, I, I, I, P, P]),
+    "ubpl_maxpool2x2_forward": (I, [P, L, I, I, P, P]),
+    "ubpl_maxpool2x2_backward": (I, [P, P, L, I, I, P, I, P]),
+    "ubpl_avgpool2x2_forward": (I, [P, L, I, I, P, P]),
+    "ubpl_avgpool2x2_backward": (I, [P, L, I, I, P, I, P]),
+    "ubpl_upsample2x_add_forward": (I, [P, P, L, I, I, P, P]),
+    "ubpl_upsample2x_add_backward": (I, [P, L, I, I, P, I, P]),
+    "ubpl_add": (I, [P, P, L, P, P]),
+}
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load the library and bind every symbol (raises if any is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError("ubpl_amd: %s not found — build it with `make -C ubpl-poseestimation_amd/csrc` "
+                           "(or __graft_entry__.build()); there is no CPU fallback" % path)
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def require_gpu(t=None):
+    if not torch.cuda.is_available():
+        raise RuntimeError("ubpl_amd: the HIP hot path needs an MI355X (gfx950) GPU; no CPU fallback")
+    if t is not None and not t.is_cuda:
+        raise RuntimeError("ubpl_amd: expected a device tensor, got %s" % t.device)
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def check(rc, name):
+    if rc != 0:
+        raise RuntimeError("ubpl_amd: %s failed with hipError %d" % (name, rc))
+
+
+def call(name, *args):
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if fn.restype is I and name != "ubpl_bn_splits":
+        check(rc, name)
+    return rc

@@ -1,0 +1,530 @@
+"""Stacked hourglass on the HIP kernels (H1-H6).
+
+Drop-in for StackedHourglass / pose_model / PoseModel
+(models/pose/hourglass.py:7-99, models/pose/pose_model.py:5-13,
+models/__init__.py:4):
+
+* the module tree, parameter names and order, buffer names, shapes and the
+  default initialisation are the reference's (so torch.manual_seed(s) gives
+  bit-identical weights, and state_dict() interchanges with reference
+  checkpoints);
+* every parameter is an alias into ONE flat device buffer (`flat_params`,
+  grad-carrying parameters first, the never-trained skip_layer parameters of
+  identity Residuals last), gradients accumulate into `flat_grads`, BN
+  running statistics live in `flat_stats` — so the EMA teacher update, the
+  optimizer step and the DDP all-reduce are each a single kernel / collective
+  over a contiguous buffer;
+* forward/backward are explicit executors over the HIP kernels (conv.hip with
+  the pre-activation BN+ReLU fused into operand staging, bn.hip, pool.hip);
+  autograd sees the whole network as one Function.
+"""
+import math
+
+import torch
+from torch import nn
+
+from . import _lib
+from . import kernels as Kn
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+# ---------------------------------------------------------------------------
+# Parameter table in the reference's registration order
+# ---------------------------------------------------------------------------
+def build_table(k, nstack):
+    """[(name, shape, kind, live)] kind in {'cw','cb','bw','bb'}; live=False for the
+    skip_layer of Residual(c, c) (constructed, never used: models/base/layers.py:63-67)."""
+    tab = []
+
+    def conv(p, cin, cout, ks, live=True):
+        tab.append((p + ".weight", (cout, cin, ks, ks), "cw", live))
+        tab.append((p + ".bias", (cout,), "cb", live))
+
+    def bn(p, c):
+        tab.append((p + ".weight", (c,), "bw", True))
+        tab.append((p + ".bias", (c,), "bb", True))
+
+    def residual(p, cin, cout):
+        half = cout // 2
+        bn(p + ".bn1", cin)
+        conv(p + ".conv1.conv", cin, half, 1)
+        bn(p + ".bn2", half)
+        conv(p + ".conv2.conv", half, half, 3)
+        bn(p + ".bn3", half)
+        conv(p + ".conv3.conv", half, cout, 1)
+        conv(p + ".skip_layer.conv", cin, cout, 1, live=cin != cout)
+
+    def hourglass(p, n, f):
+        residual(p + ".up1", f, f)
+        residual(p + ".low1", f, f)
+        if n > 1:
+            hourglass(p + ".low2", n - 1, f)
+        else:
+            residual(p + ".low2", f, f)
+        residual(p + ".low3", f, f)
+
+    conv("pre.0.conv", 3, 64, 7)
+    bn("pre.0.bn", 64)
+    residual("pre.1", 64, 128)
+    residual("pre.3", 128, 128)
+    residual("pre.4", 128, 256)
+    for i in range(nstack):
+        hourglass("hgs.%d.0" % i, 4, 256)
+    for i in range(nstack):
+        residual("features.%d.0" % i, 256, 256)
+        conv("features.%d.1.conv" % i, 256, 256, 1)
+        bn("features.%d.1.bn" % i, 256)
+    for i in range(nstack):
+        conv("preds.%d.conv" % i, 256, k, 1)
+    for i in range(nstack - 1):
+        conv("merge_features.%d.conv.conv" % i, 256, 256, 1)
+    for i in range(nstack - 1):
+        conv("merge_preds.%d.conv.conv" % i, k, 256, 1)
+    return tab
+
+
+def _default_init(tab):
+    """nn.Conv2d.reset_parameters / BatchNorm2d defaults, consuming the CPU RNG in
+    registration order exactly like the reference constructor."""
+    vals = []
+    last_w = None
+    for name, shape, kind, _ in tab:
+        t = torch.empty(shape)
+        if kind == "cw":
+            nn.init.kaiming_uniform_(t, a=math.sqrt(5))
+            last_w = t
+        elif kind == "cb":
+            fan_in, _ = nn.init._calculate_fan_in_and_fan_out(last_w)
+            bound = 1 / math.sqrt(fan_in) if fan_in > 0 else 0
+            nn.init.uniform_(t, -bound, bound)
+        elif kind == "bw":
+            t.fill_(1.0)
+        else:
+            t.zero_()
+        vals.append(t)
+    return vals
+
+
+class _Node(nn.Module):
+    """Container mirroring one module of the reference tree (params/buffers only)."""
+
+    def forward(self, *a):  # pragma: no cover - never called
+        raise RuntimeError("structural node")
+
+
+# ---------------------------------------------------------------------------
+# The model
+# ---------------------------------------------------------------------------
+class StackedHourglass(nn.Module):
+    """StackedHourglass(k, nStack, mode) on the HIP path.  forward(imgs) ->
+    preds [B,S,K,R,R] (mode 'default') or (preds, features [B,S,256,R/2,R/2])
+    for mode 'AvgPool' / 'MaxPool' (models/pose/hourglass.py:60-99).  'ConvOne'
+    builds a 128-channel conv on 256-channel features in the reference and
+    fails there; it is rejected here."""
+
+    def __init__(self, k, nStack, mode="default", device=None):
+        super().__init__()
+        if mode not in ("default", "AvgPool", "MaxPool"):
+            raise ValueError("mode %r unsupported (ConvOne is broken in the reference: hourglass.py:227)" % mode)
+        _lib.require_gpu()
+        device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.k, self.nStack, self.mode = k, nStack, mode
+        tab = build_table(k, nStack)
+        vals = _default_init(tab)          # CPU RNG, reference order
+        # flat layout: live parameters first (reference order), dead ones last
+        order = [i for i, e in enumerate(tab) if e[3]] + [i for i, e in enumerate(tab) if not e[3]]
+        offs, o = {}, 0
+        for i in order:
+            n = vals[i].numel()
+            offs[tab[i][0]] = (o, n, tab[i][1])
+            o += (n + 3) // 4 * 4          # keep every segment 16-B aligned
+        self.n_total = o
+        self.n_live = max(offs[tab[i][0]][0] + offs[tab[i][0]][1] for i in order if tab[i][3])
+        self.n_live = (self.n_live + 3) // 4 * 4
+        host = torch.zeros(self.n_total)
+        for i, e in enumerate(tab):
+            s, n, _ = offs[e[0]]
+            host[s:s + n] = vals[i].reshape(-1)
+        self.flat_params = host.to(device)
+        self.flat_grads = torch.zeros(self.n_total, device=device)
+        self._offs = offs
+        self._table = tab
+        # BN running statistics in one flat buffer: per BN [mean(C) | var(C)]
+        bns = [e[0][:-len(".weight")] for e in tab if e[2] == "bw"]
+        self._bn_names = bns
+        so, sidx = 0, {}
+        for b in bns:
+            c = offs[b + ".weight"][1]
+            sidx[b] = (so, c)
+            so += 2 * c
+        stats = torch.zeros(so)
+        for b, (s, c) in sidx.items():
+            stats[s + c:s + 2 * c] = 1.0
+        self.flat_stats = stats.to(device)
+        self._nbt = torch.zeros(len(bns), dtype=torch.long, device=device)
+        self._sidx = sidx
+        self._bn_index = {b: i for i, b in enumerate(bns)}
+        # module tree with aliased parameters / buffers, in reference order
+        for name, shape, kind, _ in tab:
+            mod, attr = self._node_for(name)
+            s, n, shp = offs[name]
+            mod.register_parameter(attr, nn.Parameter(self.flat_params[s:s + n].view(shp)))
+            if kind == "bb":
+                b = name[:-len(".bias")]
+                bs, c = sidx[b]
+                mod.register_buffer("running_mean", self.flat_stats[bs:bs + c])
+                mod.register_buffer("running_var", self.flat_stats[bs + c:bs + 2 * c])
+                mod.register_buffer("num_batches_tracked", self._nbt[self._bn_index[b]])
+        self._grad_views_attached = False
+        self._ws = {}
+
+    # -- structure helpers ------------------------------------------------
+    def _node_for(self, name):
+        parts = name.split(".")
+        mod = self
+        for p in parts[:-1]:
+            if p not in mod._modules:
+                mod.add_module(p, _Node())
+            mod = mod._modules[p]
+        return mod, parts[-1]
+
+    def _apply(self, fn, recurse=True):
+        # Parameters alias flat device buffers: only same-device no-op moves are legal.
+        probe = fn(self.flat_params)
+        if probe.device != self.flat_params.device or probe.dtype != self.flat_params.dtype:
+            raise RuntimeError("ubpl_amd StackedHourglass lives on its GPU in float32 (flat buffers); "
+                               "moving it to %s/%s is not supported" % (probe.device, probe.dtype))
+        return self
+
+    def P(self, name):
+        s, n, shp = self._offs[name]
+        return self.flat_params[s:s + n].view(shp)
+
+    def G(self, name):
+        s, n, shp = self._offs[name]
+        return self.flat_grads[s:s + n].view(shp)
+
+    def stats(self, bn):
+        s, c = self._sidx[bn]
+        return self.flat_stats[s:s + c], self.flat_stats[s + c:s + 2 * c]
+
+    def live_params(self):
+        return self.flat_params[:self.n_live]
+
+    def live_grads(self):
+        return self.flat_grads[:self.n_live]
+
+    def attach_grad_views(self):
+        """Make every parameter's .grad alias flat_grads (for torch optimizers)."""
+        for name, p in self.named_parameters():
+            if self._offs[name][0] < self.n_live:      # dead skip_layer params keep grad None
+                p.grad = self.G(name)
+        self._grad_views_attached = True
+
+    def zero_grad(self, set_to_none=True):
+        self.flat_grads.zero_()
+        self.attach_grad_views()
+
+    # -- forward ----------------------------------------------------------
+    def forward(self, imgs):
+        _lib.require_gpu(imgs)
+        if imgs.dtype != torch.float32:
+            raise TypeError("imgs must be float32")
+        imgs = imgs.contiguous()
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        if need_grad and not self.training:
+            raise RuntimeError("ubpl_amd: backward through eval-mode BatchNorm is not supported")
+        if need_grad:
+            preds, feats = _HourglassFn.apply(imgs, self._anchor(), self)
+        else:
+            with torch.no_grad():
+                preds, feats, _ = self._forward_impl(imgs, save=False)
+        if self.mode == "default":
+            return preds
+        return preds, feats
+
+    def _anchor(self):
+        a = getattr(self, "_anchor_t", None)
+        if a is None:
+            a = torch.zeros((), device=self.flat_params.device, requires_grad=True)
+            self._anchor_t = a
+        return a
+
+    def _scratch(self, B, C):
+        key = ("part", B)
+        if key not in self._ws:
+            n = 0
+            for c in (64, 128, 256, 512):
+                n = max(n, 2 * c * Kn.bn_splits(B, c))
+            self._ws[key] = torch.empty(n, dtype=torch.float64, device=self.flat_params.device)
+            self._ws[("coef", B)] = torch.empty(3 * 512, device=self.flat_params.device)
+        return self._ws[key]
+
+    def _forward_impl(self, imgs, save):
+        B = imgs.shape[0]
+        dev = imgs.device
+        part = self._scratch(B, 64)
+        ex = _Exec(self, B, dev, part, train=self.training, save=save)
+        if self.training:
+            self._nbt.add_(1)
+        else:
+            ex.eval_coeffs()
+        x = ex.stem(imgs)
+        x = ex.residual("pre.1", x)
+        x1 = x
+        x = Kn.maxpool2x2(x1)
+        ex.save("pre.2", x1)
+        x = ex.residual("pre.3", x)
+        x = ex.residual("pre.4", x)
+        preds, feats = [], []
+        for i in range(self.nStack):
+            hg = ex.hourglass("hgs.%d.0" % i, 4, x)
+            f0 = ex.residual("features.%d.0" % i, hg)
+            f = ex.conv_bn_relu("features.%d.1" % i, f0)
+            if self.mode != "default":
+                feats.append(Kn.avgpool2x2(f) if self.mode == "AvgPool" else Kn.maxpool2x2(f))
+            pr = ex.conv("preds.%d.conv" % i, f)
+            preds.append(pr)
+            if i < self.nStack - 1:
+                t = ex.conv("merge_preds.%d.conv.conv" % i, pr, res=x)
+                x = ex.conv("merge_features.%d.conv.conv" % i, f, res=t, out=t)
+            ex.save("stack.%d" % i, (f, pr))
+        P = torch.stack(preds, 1)
+        Fs = torch.stack(feats, 1) if feats else None
+        return P, Fs, ex
+
+    # -- backward ---------------------------------------------------------
+    def _backward_impl(self, ex, dpreds, dfeats):
+        ex.backward(dpreds, dfeats)
+
+
+class _HourglassFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, imgs, anchor, model):
+        preds, feats, ex = model._forward_impl(imgs, save=True)
+        ctx.ex = ex
+        ctx.model = model
+        if feats is None:
+            feats = preds.new_empty(0)
+        return preds, feats
+
+    @staticmethod
+    def backward(ctx, dpreds, dfeats):
+        model = ctx.model
+        # torch optimizers may have reset .grad to None (zero_grad(set_to_none));
+        # then the flat buffer is stale and is restarted from zero.
+        first = next(iter(model.parameters()))
+        if first.grad is None or first.grad.data_ptr() != model.flat_grads.data_ptr() + 4 * model._offs[
+                model._table[0][0]][0]:
+            model.flat_grads.zero_()
+            model.attach_grad_views()
+        if dfeats is not None and dfeats.numel() == 0:
+            dfeats = None
+        model._backward_impl(ctx.ex, dpreds, dfeats)
+        ctx.ex = None
+        return None, None, None
+
+
+# ---------------------------------------------------------------------------
+# Executor: one forward pass (+ its saved tensors) and its backward
+# ---------------------------------------------------------------------------
+class _Exec:
+    def __init__(self, model, B, dev, part, train, save):
+        self.m, self.B, self.dev, self.part, self.train, self.do_save = model, B, dev, part, train, save
+        self.saved = {}
+        C = sum(self.m._offs[b + ".weight"][1] for b in self.m._bn_names)
+        self.coef = torch.empty(4 * C, device=dev)     # per BN: scale|shift|mean|invstd
+        self.cidx, o = {}, 0
+        for b in self.m._bn_names:
+            c = self.m._offs[b + ".weight"][1]
+            self.cidx[b] = (o, c)
+            o += 4 * c
+
+    # ---- bookkeeping
+    def save(self, key, val):
+        if self.do_save:
+            self.saved[key] = val
+
+    def bnc(self, bn):
+        o, c = self.cidx[bn]
+        v = self.coef[o:o + 4 * c]
+        return v[:c], v[c:2 * c], v[2 * c:3 * c], v[3 * c:]
+
+    def eval_coeffs(self):
+        for b in self.m._bn_names:
+            sc, sh, _, _ = self.bnc(b)
+            rm, rv = self.m.stats(b)
+            Kn.bn_eval_coeffs(self.m.P(b + ".weight"), self.m.P(b + ".bias"), rm, rv, BN_EPS, sc, sh)
+
+    def bn(self, name, x):
+        """Train: batch statistics (+ running-stat update); eval: precomputed."""
+        sc, sh, mu, istd = self.bnc(name)
+        if self.train:
+            rm, rv = self.m.stats(name)
+            Kn.bn_forward_stats(x, self.m.P(name + ".weight"), self.m.P(name + ".bias"), BN_EPS, BN_MOMENTUM, rm,
+                                rv, self.part, mu, istd, sc, sh)
+        return sc, sh
+
+    def conv(self, name, x, stride=1, pro=None, res=None, out=None):
+        w = self.m.P(name + ".weight")
+        b = self.m.P(name + ".bias")
+        ps, ph = (None, None) if pro is None else pro
+        return Kn.conv2d_forward(x, w, b, stride, ps, ph, res=res, out=out)
+
+    # ---- layers
+    def stem(self, imgs):
+        y0 = self.conv("pre.0.conv", imgs, stride=2)
+        sc, sh = self.bn("pre.0.bn", y0)
+        x0 = Kn.bn_apply(y0, sc, sh, relu=1)
+        self.save("pre.0", (imgs, y0))
+        return x0
+
+    def conv_bn_relu(self, p, x):
+        y = self.conv(p + ".conv", x)
+        sc, sh = self.bn(p + ".bn", y)
+        f = Kn.bn_apply(y, sc, sh, relu=1)
+        self.save(p, (x, y))
+        return f
+
+    def residual(self, p, x):
+        """models/base/layers.py:69-84 (pre-activation bottleneck)."""
+        cin = x.shape[1]
+        cout = self.m._offs[p + ".conv3.conv.weight"][2][0]
+        c1 = self.bn(p + ".bn1", x)
+        t1 = self.conv(p + ".conv1.conv", x, pro=c1)
+        c2 = self.bn(p + ".bn2", t1)
+        t2 = self.conv(p + ".conv2.conv", t1, pro=c2)
+        c3 = self.bn(p + ".bn3", t2)
+        if cin != cout:
+            r = self.conv(p + ".skip_layer.conv", x)
+            out = self.conv(p + ".conv3.conv", t2, pro=c3, res=r, out=r)
+        else:
+            out = self.conv(p + ".conv3.conv", t2, pro=c3, res=x)
+        self.save(p, (x, t1, t2))
+        return out
+
+    def hourglass(self, p, n, x):
+        """models/base/layers.py:104-111."""
+        up1 = self.residual(p + ".up1", x)
+        pl = Kn.maxpool2x2(x)
+        low1 = self.residual(p + ".low1", pl)
+        low2 = self.hourglass(p + ".low2", n - 1, low1) if n > 1 else self.residual(p + ".low2", low1)
+        low3 = self.residual(p + ".low3", low2)
+        self.save(p, x)
+        return Kn.upsample2x_add(up1, low3, out=up1)
+
+    # ---- backward
+    def _coef(self):
+        return self.m._ws[("coef", self.B)]
+
+    def bn_bwd(self, name, dz, x, relu, add1=None, add2=None, out=None):
+        sc, sh, mu, istd = self.bnc(name)
+        return Kn.bn_backward(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.part, self._coef(),
+                              self.m.G(name + ".weight"), self.m.G(name + ".bias"), add1=add1, add2=add2, out=out)
+
+    def wgrad(self, name, dy, x, KS, stride=1, pro=None):
+        ps, ph = (None, None) if pro is None else pro
+        Kn.conv2d_wgrad(dy, x, KS, stride, self.m.G(name + ".weight"), self.m.G(name + ".bias"), ps, ph,
+                        accumulate=True)
+
+    def dgrad(self, name, dy, res=None, out=None):
+        return Kn.conv2d_dgrad(dy, self.m.P(name + ".weight"), res=res, out=out)
+
+    def residual_bwd(self, p, dout):
+        x, t1, t2 = self.saved.get(p)
+        cin = x.shape[1]
+        cout = dout.shape[1]
+        c1 = self.bnc(p + ".bn1")[:2]
+        c2 = self.bnc(p + ".bn2")[:2]
+        c3 = self.bnc(p + ".bn3")[:2]
+        self.wgrad(p + ".conv3.conv", dout, t2, 1, pro=c3)
+        d = self.dgrad(p + ".conv3.conv", dout)                       # d relu(bn3(t2))
+        d = self.bn_bwd(p + ".bn3", d, t2, relu=1)                     # d t2
+        self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
+        d = self.dgrad(p + ".conv2.conv", d)                           # d relu(bn2(t1))
+        d = self.bn_bwd(p + ".bn2", d, t1, relu=1)                     # d t1
+        self.wgrad(p + ".conv1.conv", d, x, 1, pro=c1)
+        d = self.dgrad(p + ".conv1.conv", d)                           # d relu(bn1(x))
+        if cin != cout:
+            self.wgrad(p + ".skip_layer.conv", dout, x, 1)
+            ds = self.dgrad(p + ".skip_layer.conv", dout)
+            return self.bn_bwd(p + ".bn1", d, x, relu=1, add1=ds)
+        return self.bn_bwd(p + ".bn1", d, x, relu=1, add1=dout)
+
+    def hourglass_bwd(self, p, n, dout):
+        x = self.saved.get(p)
+        B, C, H, W = dout.shape
+        dlow3 = torch.empty((B, C, H // 2, W // 2), device=self.dev)
+        Kn.upsample2x_add_backward(dout, dlow3, accumulate=False)
+        dlow2 = self.residual_bwd(p + ".low3", dlow3)
+        dlow1 = self.hourglass_bwd(p + ".low2", n - 1, dlow2) if n > 1 else self.residual_bwd(p + ".low2", dlow2)
+        dpl = self.residual_bwd(p + ".low1", dlow1)
+        dx = self.residual_bwd(p + ".up1", dout)
+        Kn.maxpool2x2_backward(x, dpl, dx, accumulate=True)
+        return dx
+
+    def backward(self, dpreds, dfeats):
+        m = self.m
+        S = m.nStack
+        dpreds = dpreds.contiguous()
+        if dfeats is not None:
+            dfeats = dfeats.contiguous()
+        dxn = None                                       # grad of the x entering stack i+1
+        for i in reversed(range(S)):
+            f, pr = self.saved.get("stack.%d" % i)
+            dpi = dpreds[:, i].contiguous()
+            if i < S - 1:
+                nmf, nmp = "merge_features.%d.conv.conv" % i, "merge_preds.%d.conv.conv" % i
+                self.wgrad(nmf, dxn, f, 1)
+                self.wgrad(nmp, dxn, pr, 1)
+                dpi = self.dgrad(nmp, dxn, res=dpi, out=dpi)
+            npd = "preds.%d.conv" % i
+            self.wgrad(npd, dpi, f, 1)
+            df = self.dgrad(npd, dpi)
+            if i < S - 1:
+                df = self.dgrad(nmf, dxn, res=df, out=df)
+            if dfeats is not None:
+                dfi = dfeats[:, i].contiguous()
+                if m.mode == "AvgPool":
+                    Kn.avgpool2x2_backward(dfi, df, accumulate=True)
+                else:
+                    Kn.maxpool2x2_backward(f, dfi, df, accumulate=True)
+            f0, yf = self.saved.get("features.%d.1" % i)
+            d = self.bn_bwd("features.%d.1.bn" % i, df, yf, relu=1)
+            self.wgrad("features.%d.1.conv" % i, d, f0, 1)
+            d = self.dgrad("features.%d.1.conv" % i, d)
+            d = self.residual_bwd("features.%d.0" % i, d)
+            dx = self.hourglass_bwd("hgs.%d.0" % i, 4, d)
+            if dxn is not None:
+                dx = Kn.add(dx, dxn, out=dx)
+            dxn = dx
+        d = self.residual_bwd("pre.4", dxn)
+        d = self.residual_bwd("pre.3", d)
+        x1 = self.saved.get("pre.2")
+        dx1 = torch.zeros_like(x1)
+        Kn.maxpool2x2_backward(x1, d, dx1, accumulate=False)
+        d = self.residual_bwd("pre.1", dx1)
+        imgs, y0 = self.saved.get("pre.0")
+        d = self.bn_bwd("pre.0.bn", d, y0, relu=1)
+        self.wgrad("pre.0.conv", d, imgs, 7, stride=2)
+
+
+def pose_model(modelType, kpsCount, mode="default", nograd=False):
+    """models/pose/pose_model.py:5-13 ('HG<n>' only; LitePose is out of scope)."""
+    if "HG" not in modelType:
+        raise ValueError("only HG<n> models are on the HIP path (got %r)" % modelType)
+    model = StackedHourglass(kpsCount, int(modelType[len("HG"):]), mode)
+    if nograd:
+        for p in model.parameters():
+            p.detach_()
+    return model
+
+
+PoseModel = pose_model
+
+
+def hg(k, nStack=3, mode="default", nograd=False):
+    """models/pose/hourglass.py:102-107."""
+    return pose_model("HG%d" % nStack, k, mode, nograd)

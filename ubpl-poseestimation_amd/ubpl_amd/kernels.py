@@ -1,0 +1,312 @@
+"""Tensor-level wrappers over the C-ABI (no autograd here).
+
+Each wrapper validates device / dtype / contiguity, allocates outputs with
+the torch caching allocator on the input's device and enqueues on torch's
+current stream.  Nothing here computes on the host.
+"""
+import torch
+
+from . import _lib
+from ._lib import call, stream
+
+F32 = torch.float32
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _chk(t, name, dtype=F32):
+    if t is None:
+        return
+    _lib.require_gpu(t)
+    if t.dtype != dtype:
+        raise TypeError("ubpl_amd: %s must be %s, got %s" % (name, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise ValueError("ubpl_amd: %s must be contiguous" % name)
+
+
+# ------------------------------------------------------------------ R1
+def render_heatmaps(kps, img_hw, inp_res, out_res, kernel_size=3.0, sigma=1.0, cutoff=0.01, kps_out=None):
+    """kps [N,K,3] -> (hm [N,K,Rh,Rw], kps_out [N,K,3] with vis applied)."""
+    _chk(kps, "kps")
+    N, K, _ = kps.shape
+    stride = inp_res / out_res
+    rh, rw = int(img_hw[0] / stride), int(img_hw[1] / stride)
+    hm = torch.empty((N, K, rh, rw), device=kps.device, dtype=F32)
+    if kps_out is None:
+        kps_out = torch.empty_like(kps)
+    call("ubpl_render_heatmaps", _p(kps), _p(hm), _p(kps_out), N, K, int(img_hw[0]), int(img_hw[1]),
+         int(inp_res), int(out_res), float(kernel_size), float(sigma), float(cutoff), stream())
+    return hm, kps_out
+
+
+# ------------------------------------------------------------------ L1-L4
+class RowGeom:
+    """Row geometry of a (pred, target) pair for the heatmap loss kernels.
+    a rows (b,s,k): a + b*a_sb + s*a_ss + k*HW; target rows: mean over m of
+    t + m*t_sm + b*t_sb + s*t_ss + k*HW (strides in elements)."""
+
+    def __init__(self, a, a_sb, a_ss, t, t_sb, t_ss, t_sm, M, B, S, K, HW):
+        self.a, self.t = a, t
+        self.a_off = 0
+        self.args = (a_sb, a_ss, t_sb, t_ss, t_sm, M, B, S, K, HW)
+        self.B, self.S, self.K, self.HW = B, S, K, HW
+        self.a_ptr = a.data_ptr()
+        self.t_ptr = t.data_ptr()
+
+
+def geom_stack(a, t, S, t_mode):
+    """a: [B,S,K,R,R] (or [B,K,R,R] with S==1), contiguous.
+    t_mode 'gt'    t [B,K,R,R] broadcast over stacks;
+           'same'  t has a's layout;
+           'ens'   t [M,B,St,K,R,R] (or [M,B,K,R,R]): mean over M of the LAST stack."""
+    _chk(a, "preds")
+    _chk(t, "targets")
+    B = a.shape[0]
+    K = a.shape[-3]
+    HW = a.shape[-1] * a.shape[-2]
+    a_sb, a_ss = S * K * HW, K * HW
+    if t_mode == "gt":
+        return RowGeom(a, a_sb, a_ss, t, K * HW, 0, 0, 1, B, S, K, HW)
+    if t_mode == "same":
+        return RowGeom(a, a_sb, a_ss, t, a_sb, a_ss, 0, 1, B, S, K, HW)
+    M = t.shape[0]
+    St = t.shape[2] if t.dim() == 6 else 1
+    g = RowGeom(a, a_sb, a_ss, t, St * K * HW, 0, B * St * K * HW, M, B, S, K, HW)
+    g.t_ptr = t.data_ptr() + (St - 1) * K * HW * 4
+    return g
+
+
+def geom_rows(a, a_base_elems, a_sb, t, t_base_elems, t_sb, B, K, HW, t_sm=0, M=1):
+    """Single-stack rows with explicit base offsets/strides (e.g. last-stack slices)."""
+    g = RowGeom(a, a_sb, 0, t, t_sb, 0, t_sm, M, B, 1, K, HW)
+    g.a_ptr = a.data_ptr() + 4 * a_base_elems
+    g.t_ptr = t.data_ptr() + 4 * t_base_elems
+    return g
+
+
+def row_stats(g, want_amax=False, want_tmax=False):
+    dev = g.a.device
+    rows = g.B * g.S * g.K
+    sq = torch.empty(rows, device=dev, dtype=F32)
+    am = torch.empty(rows, device=dev, dtype=F32) if want_amax else None
+    tm = torch.empty(rows, device=dev, dtype=F32) if want_tmax else None
+    a_sb, a_ss, t_sb, t_ss, t_sm, M, B, S, K, HW = g.args
+    call("ubpl_heatmap_row_stats", g.a_ptr, a_sb, a_ss, g.t_ptr, t_sb, t_ss, t_sm, M, B, S, K, HW,
+         _p(sq), _p(am), _p(tm), stream())
+    return sq, am, tm
+
+
+def loss_finalize(kind, sq, amax, tmax, gate, sw, use_gate, use_sw, B, S, K, thr):
+    dev = sq.device
+    out_sum = torch.empty(1, device=dev, dtype=F32)
+    out_cnt = torch.empty(4, device=dev, dtype=torch.int32)
+    score = torch.empty(K, device=dev, dtype=F32) if kind != 0 else None
+    w = torch.empty(B * S * K, device=dev, dtype=F32)
+    call("ubpl_loss_finalize", int(kind), _p(sq), _p(amax), _p(tmax), _p(gate), _p(sw), int(use_gate),
+         int(use_sw), B, S, K, float(thr), _p(out_sum), _p(out_cnt), _p(score), _p(w), stream())
+    return out_sum, out_cnt, score, w
+
+
+def row_grad(g, w, gscale, extra, da, accumulate=False):
+    a_sb, a_ss, t_sb, t_ss, t_sm, M, B, S, K, HW = g.args
+    call("ubpl_heatmap_row_grad", g.a_ptr, a_sb, a_ss, g.t_ptr, t_sb, t_ss, t_sm, M, B, S, K, HW, _p(w),
+         _p(gscale), float(extra), _p(da), int(accumulate), stream())
+    return da
+
+
+# ------------------------------------------------------------------ L5
+def fdl_cov_forward(f1, f2, rowmask=None):
+    _chk(f1, "f1")
+    _chk(f2, "f2")
+    B, S, C = f1.shape[:3]
+    HW = f1[0, 0, 0].numel()
+    dev = f1.device
+    cov = torch.empty(B * S * C, device=dev, dtype=F32)
+    mu1, mu2 = torch.empty_like(cov), torch.empty_like(cov)
+    val = torch.empty(1, device=dev, dtype=F32)
+    cnt = torch.empty(1, device=dev, dtype=torch.int32)
+    call("ubpl_fdl_cov_forward", _p(f1), _p(f2), _p(rowmask), B, S, C, HW, _p(cov), _p(mu1), _p(mu2), _p(val),
+         _p(cnt), stream())
+    return val, cnt, (cov, mu1, mu2)
+
+
+def fdl_cov_backward(f1, f2, rowmask, saved, cnt, gscale, d1=None, d2=None, accumulate=False):
+    B, S, C = f1.shape[:3]
+    HW = f1[0, 0, 0].numel()
+    cov, mu1, mu2 = saved
+    call("ubpl_fdl_cov_backward", _p(f1), _p(f2), _p(rowmask), _p(cov), _p(mu1), _p(mu2), _p(cnt), _p(gscale),
+         B, S, C, HW, _p(d1), _p(d2), int(accumulate), stream())
+    return d1, d2
+
+
+# ------------------------------------------------------------------ D1-D4
+def decode_heatmaps(hm, tinv=None):
+    """hm [N,K,H,W] -> (raw [N,K,2], preds [N,K,2] or None, scores [N,K])."""
+    _chk(hm, "heatmap")
+    N, K, H, W = hm.shape
+    dev = hm.device
+    raw = torch.empty((N, K, 2), device=dev, dtype=F32)
+    preds = torch.empty((N, K, 2), device=dev, dtype=F32) if tinv is not None else None
+    scores = torch.empty((N, K), device=dev, dtype=F32)
+    if tinv is not None:
+        _chk(tinv, "tinv", torch.float64)
+    call("ubpl_decode_heatmaps", _p(hm), N, K, H, W, _p(tinv), _p(raw), _p(preds), _p(scores), stream())
+    return raw, preds, scores
+
+
+def pck(preds, gts, ref, thr):
+    _chk(preds, "preds")
+    _chk(gts, "gts")
+    N, K, _ = preds.shape
+    dev = preds.device
+    errs = torch.empty(K + 1, device=dev, dtype=F32)
+    accs = torch.empty(K + 1, device=dev, dtype=F32)
+    hits = torch.empty(K, device=dev, dtype=torch.int32)
+    valid = torch.empty(K, device=dev, dtype=torch.int32)
+    call("ubpl_pck", _p(preds), _p(gts), N, K, int(ref[0]), int(ref[1]), float(thr), _p(errs), _p(accs), _p(hits),
+         _p(valid), stream())
+    return errs, accs, hits, valid
+
+
+# ------------------------------------------------------------------ E1
+def ema_update_(ema, p, alpha):
+    _chk(ema, "ema")
+    _chk(p, "param")
+    assert ema.numel() == p.numel()
+    call("ubpl_ema_update", _p(ema), _p(p), ema.numel(), float(alpha), stream())
+
+
+def adamw_step_(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step):
+    for t, n in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
+        _chk(t, n)
+    call("ubpl_adamw_step", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
+         float(eps), float(weight_decay), int(step), stream())
+
+
+def scale_(x, s):
+    _chk(x, "x")
+    call("ubpl_scale_", _p(x), x.numel(), float(s), stream())
+
+
+# ------------------------------------------------------------------ BN
+def bn_splits(B, C):
+    return _lib.lib().ubpl_bn_splits(B, C)
+
+
+def bn_forward_stats(x, gamma, beta, eps, momentum, rmean, rvar, part, mean, invstd, scale, shift):
+    B, C = x.shape[:2]
+    HW = x[0, 0].numel()
+    call("ubpl_bn_forward_stats", _p(x), B, C, HW, _p(gamma), _p(beta), float(eps), float(momentum), _p(rmean),
+         _p(rvar), _p(part), _p(mean), _p(invstd), _p(scale), _p(shift), stream())
+
+
+def bn_eval_coeffs(gamma, beta, rmean, rvar, eps, scale, shift):
+    call("ubpl_bn_eval_coeffs", _p(gamma), _p(beta), _p(rmean), _p(rvar), float(eps), gamma.numel(), _p(scale),
+         _p(shift), stream())
+
+
+def bn_apply(x, scale, shift, relu, out=None):
+    B, C = x.shape[:2]
+    HW = x[0, 0].numel()
+    y = torch.empty_like(x) if out is None else out
+    call("ubpl_bn_apply", _p(x), B, C, HW, _p(scale), _p(shift), int(relu), _p(y), stream())
+    return y
+
+
+def bn_backward(dz, x, gamma, mean, invstd, scale, shift, relu, part, coef, dgamma, dbeta, add1=None, add2=None,
+                out=None):
+    B, C = x.shape[:2]
+    HW = x[0, 0].numel()
+    dx = dz if out is None else out
+    call("ubpl_bn_backward", _p(dz), _p(x), B, C, HW, _p(gamma), _p(mean), _p(invstd), _p(scale), _p(shift),
+         int(relu), _p(part), _p(coef), _p(dgamma), _p(dbeta), _p(add1), _p(add2), _p(dx), stream())
+    return dx
+
+
+# ------------------------------------------------------------------ conv
+def conv_out_hw(H, W, KS, stride):
+    pad = (KS - 1) // 2
+    return (H + 2 * pad - KS) // stride + 1, (W + 2 * pad - KS) // stride + 1
+
+
+def conv2d_forward(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out=None):
+    B, Cin, H, W = x.shape
+    Cout, wc, KS, _ = w.shape
+    if wc != Cin:
+        raise AssertionError("{} {}".format(Cin, wc))  # models/base/layers.py:44
+    Ho, Wo = conv_out_hw(H, W, KS, stride)
+    y = torch.empty((B, Cout, Ho, Wo), device=x.device, dtype=F32) if out is None else out
+    call("ubpl_conv2d_forward", _p(x), B, Cin, H, W, _p(w), _p(bias), Cout, KS, stride, _p(pscale), _p(pshift),
+         _p(res), _p(y), Ho, Wo, stream())
+    return y
+
+
+def conv2d_wgrad(dy, x, KS, stride, dw, db, pscale=None, pshift=None, accumulate=True):
+    B, Cin, H, W = x.shape
+    Cout, Ho, Wo = dy.shape[1], dy.shape[2], dy.shape[3]
+    n = _lib.lib().ubpl_conv2d_wgrad_workspace(B, Cin, Cout, KS, Ho, Wo)
+    slab = torch.empty(int(n), device=x.device, dtype=F32)
+    call("ubpl_conv2d_wgrad", _p(dy), _p(x), B, Cin, H, W, Cout, KS, stride, _p(pscale), _p(pshift), Ho, Wo,
+         _p(slab), _p(dw), _p(db), int(accumulate), stream())
+
+
+def conv_weight_flip(w):
+    Cout, Cin, KS, _ = w.shape
+    wt = torch.empty((Cin, Cout, KS, KS), device=w.device, dtype=F32)
+    call("ubpl_conv_weight_flip", _p(w), Cout, Cin, KS, _p(wt), stream())
+    return wt
+
+
+def conv2d_dgrad(dy, w, res=None, out=None, wt=None):
+    """dx of a stride-1 conv = conv(dy, flip(w)^T); res/out allow accumulation."""
+    if wt is None:
+        wt = conv_weight_flip(w)
+    return conv2d_forward(dy, wt, None, 1, res=res, out=out)
+
+
+# ------------------------------------------------------------------ pool / upsample
+def maxpool2x2(x, out=None):
+    B, C, H, W = x.shape
+    y = torch.empty((B, C, H // 2, W // 2), device=x.device, dtype=F32) if out is None else out
+    call("ubpl_maxpool2x2_forward", _p(x), B * C, H, W, _p(y), stream())
+    return y
+
+
+def maxpool2x2_backward(x, dy, dx, accumulate):
+    B, C, H, W = x.shape
+    call("ubpl_maxpool2x2_backward", _p(x), _p(dy), B * C, H, W, _p(dx), int(accumulate), stream())
+    return dx
+
+
+def avgpool2x2(x, out=None):
+    B, C, H, W = x.shape
+    y = torch.empty((B, C, H // 2, W // 2), device=x.device, dtype=F32) if out is None else out
+    call("ubpl_avgpool2x2_forward", _p(x), B * C, H, W, _p(y), stream())
+    return y
+
+
+def avgpool2x2_backward(dy, dx, accumulate):
+    B, C, H, W = dx.shape
+    call("ubpl_avgpool2x2_backward", _p(dy), B * C, H, W, _p(dx), int(accumulate), stream())
+    return dx
+
+
+def upsample2x_add(up, low, out=None):
+    B, C, H, W = up.shape
+    y = torch.empty_like(up) if out is None else out
+    call("ubpl_upsample2x_add_forward", _p(up), _p(low), B * C, H, W, _p(y), stream())
+    return y
+
+
+def upsample2x_add_backward(dout, dlow, accumulate):
+    B, C, H, W = dout.shape
+    call("ubpl_upsample2x_add_backward", _p(dout), B * C, H, W, _p(dlow), int(accumulate), stream())
+    return dlow
+
+
+def add(a, b, out=None):
+    y = torch.empty_like(a) if out is None else out
+    call("ubpl_add", _p(a), _p(b), a.numel(), _p(y), stream())
+    return y
