@@ -1,0 +1,237 @@
+"""Benchmark: MT_UBPL training step (2-stack hourglass, 256x256, K=16,
+B=32 per GPU: 16 unlabeled + 16 labeled rows) on the HIP path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+One step = what projects/MT_UBPL.py:173-339 does for one batch: heatmap
+targets rendered on the device from keypoints, 2 students x 2 views
+forward+backward, 2 teachers x 2 views forward (train-mode BN), the MSE /
+consistency / UBPL pseudo-label / FDL losses, two AdamW steps, two EMA
+updates — and under torch.distributed the global-count all-reduce and the
+student-gradient all-reduce.  Inputs (images, keypoints) are synthetic and
+already resident in HBM when timing starts.
+
+Rank 0 prints ONE JSON line (see the driver contract in the task notes):
+value = images/s over all ranks, plus `roofline` for the dominant kernel
+(the 3x3 implicit-GEMM conv forward on the f32 matrix cores, timed per
+launch with HIP events on its stream inside the timed region) and
+`cpu_baseline` (the oracle's CPU restatement of the same step on a bounded
+sample, host threads stated).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+import types
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ubpl-poseestimation_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec training step (MT_UBPL, 2-stack HG, 256×256) at 1/2/4/8 GPUs; PCK@0.2"
+MEANS = [0.4920829, 0.4920829, 0.4920829]
+F32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+
+
+def make_args(B):
+    return types.SimpleNamespace(
+        nStack=2, pseudoScoreThr=0.95, ensemblePseudoWeight=10.0, consWeight=10.0, poseWeight=10.0,
+        FDLWeight=1.0, FDL_label="labeled", FDL_type="covariance", epo=1, ema_decay=0.999, pseudoWeight=1.0,
+        outRes=64, lr=2.5e-4, wd=0.0, feature_mode="AvgPool")
+
+
+def make_batches(n, B, K, dev, seed):
+    """Synthetic batches resident on the device: images
+    U[0,1) minus the Mouse means, integer keypoints in [8, 248), unlabeled
+    rows first and zeroed (TwoStreamBatchSampler order)."""
+    g = torch.Generator().manual_seed(seed)
+    nlab = B // 2
+    out = []
+    means = torch.tensor(MEANS)[None, :, None, None]
+    for _ in range(n):
+        imgs, kps = [], []
+        isl = torch.tensor([0] * (B - nlab) + [1] * nlab, dtype=torch.bool)
+        for _a in range(2):
+            imgs.append((torch.rand(B, 3, 256, 256, generator=g) - means).to(dev))
+            k = torch.zeros(B, K, 3)
+            k[:, :, :2] = torch.randint(8, 248, (B, K, 2), generator=g).float()
+            k[:, :, 2] = 1.0
+            k[~isl] = 0.0
+            kps.append(k.to(dev))
+        out.append((imgs, None, {"kps": kps, "islabeled": [isl.to(dev)]}))
+    return out
+
+
+class ConvTimer:
+    """Wraps kernels.conv2d_forward: HIP events around every 3x3 forward launch
+    (on the current stream, which the kernel is launched on)."""
+
+    def __init__(self, Kn):
+        self.Kn = Kn
+        self.orig = Kn.conv2d_forward
+        self.events = []
+        self.flops = 0
+        self.active = False
+
+    def __enter__(self):
+        orig = self.orig
+
+        def wrapped(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out=None):
+            if not self.active or w.shape[-1] != 3 or pscale is None:
+                return orig(x, w, bias, stride, pscale, pshift, res, out)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            y = orig(x, w, bias, stride, pscale, pshift, res, out)
+            e.record()
+            self.events.append((s, e))
+            B, Cin = x.shape[:2]
+            Cout = w.shape[0]
+            self.flops += 2 * B * Cout * Cin * 9 * y.shape[-1] * y.shape[-2]
+            return y
+        self.Kn.conv2d_forward = wrapped
+        return self
+
+    def __exit__(self, *a):
+        self.Kn.conv2d_forward = self.orig
+
+    def result(self):
+        torch.cuda.synchronize()
+        n = len(self.events)
+        if n == 0:
+            return None
+        ms = sum(s.elapsed_time(e) for s, e in self.events)
+        avg_ms = ms / n
+        flops_per_launch = self.flops / n
+        achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "kernel": "conv_fwd_kernel<3x3,f32 MFMA> (Residual conv2)", "launches": n,
+                "avg_launch_us": round(avg_ms * 1e3, 2), "flops_per_launch": int(flops_per_launch)}
+
+
+def cpu_baseline(steps=2, B=4):
+    """The oracle's CPU restatement of the same MT_UBPL step (oracle/step.py),
+    timed on this host's cores on a bounded sample."""
+    from oracle import hourglass as OH
+    from oracle import render as OR
+    from oracle import step as OS
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(1388)
+    models, emas, optims = [], [], []
+    for _ in range(2):
+        models.append(OH.oracle_factory(16, 2, "AvgPool"))
+        e = OH.oracle_factory(16, 2, "AvgPool")
+        e.requires_grad_(False)
+        emas.append(e)
+        optims.append(torch.optim.AdamW(models[-1].parameters(), lr=2.5e-4, weight_decay=0))
+    args = make_args(B)
+    args.nStack = 2
+    batches = []
+    for (imgs, _, meta) in make_batches(steps + 1, B, 16, "cpu", 77):
+        hms, gates = [], []
+        for k in meta["kps"]:
+            h, kk = OR.render_batch(k.numpy(), (256, 256), 256, 64)
+            hms.append([torch.from_numpy(h)])
+            gates.append([torch.from_numpy(kk[:, :, 2].copy())])
+        batches.append((imgs, hms, {"kpsWeights": gates, "islabeled": meta["islabeled"]}))
+    OS.train_mt_ubpl(batches[:1], models, emas, optims, args)      # warm-up
+    t = time.time()
+    OS.train_mt_ubpl(batches[1:], models, emas, optims, args)
+    dt = time.time() - t
+    return {"value": round(steps * B / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": "oracle/step.py MT_UBPL step (same math as projects/MT_UBPL.py:157), 2-stack, "
+                      "B=%d (half labeled), 256x256, K=16, %d timed steps, torch CPU fp32" % (B, steps)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from ubpl_amd import _lib, kernels as Kn
+    from ubpl_amd.hourglass import StackedHourglass
+    from ubpl_amd.optim import FlatAdamW
+    from ubpl_amd import train as T
+    from ubpl_amd import dist as D
+    _lib.load()
+
+    B, K = a.batch, 16
+    torch.manual_seed(1388)
+    models, emas, optims = [], [], []
+    for _ in range(2):                               # projects/MT_UBPL.py:43-50
+        m = StackedHourglass(K, 2, "AvgPool")
+        e = StackedHourglass(K, 2, "AvgPool")
+        for p in e.parameters():
+            p.detach_()
+        models.append(m)
+        emas.append(e)
+        optims.append(FlatAdamW(m, lr=2.5e-4, weight_decay=0.0))
+    D.broadcast_params(models + emas)
+    args = make_args(B)
+    batches = make_batches(2, B, K, dev, 1388 + rank)
+    warm = [batches[i % 2] for i in range(a.warmup)]
+    timed = [batches[i % 2] for i in range(a.steps)]
+
+    T.train_mt_ubpl(warm, models, emas, optims, args, verbose=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    with ConvTimer(Kn) as ct:
+        ct.active = True
+        t0 = time.perf_counter()
+        T.train_mt_ubpl(timed, models, emas, optims, args, verbose=False)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        ct.active = False
+    roof = ct.result()
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    images = world * B * a.steps
+    if rank == 0:
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline()
+        line = {
+            "metric": METRIC, "value": round(images / dt, 3), "unit": "images/sec", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (U[0,1) images - means, integer keypoints, half labeled; heatmaps rendered on device)",
+            "config": {"workload": "MT_UBPL train step, 2 students + 2 EMA teachers, 2 views",
+                       "model": "StackedHourglass HG2 (K=16, AvgPool features)", "global_batch": B * world,
+                       "per_gpu_batch": B, "input": "256x256x3", "heatmap": "16x64x64",
+                       "parallelism": "dp%d" % world},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

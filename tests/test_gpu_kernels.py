@@ -325,14 +325,17 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(case):
     xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
     scd, shd = (sc.to(DEV), sh.to(DEV)) if pro else (None, None)
     yd = Kn.conv2d_forward(xd, wd, bd, st, scd, shd, res=res.to(DEV) if resid else None)
-    _close(yd, yref, rtol=1e-4, atol=2e-5)
+    # exact-f32 MFMA chains vs MKL: elementwise within 1e-4 relative, or 1e-5 of
+    # the tensor's scale for elements near a cancellation to ~0
+    sc_ = lambda t: 1e-5 * float(t.abs().max())
+    _close(yd, yref, rtol=1e-4, atol=sc_(yref))
     dw, db = torch.zeros_like(wd), torch.zeros_like(bd)
     Kn.conv2d_wgrad(dy.to(DEV), xd, KS, st, dw, db, scd, shd, accumulate=True)
-    _close(dw, wr.grad, rtol=1e-4, atol=1e-4)
-    _close(db, br.grad, rtol=1e-4, atol=1e-4)
+    _close(dw, wr.grad, rtol=1e-4, atol=sc_(wr.grad))
+    _close(db, br.grad, rtol=1e-4, atol=sc_(br.grad))
     if st == 1:
         # dgrad w.r.t. the conv input (after the prologue)
         inp_r = inp.detach().clone().requires_grad_(True)
         F.conv2d(inp_r, w, b, st, (KS - 1) // 2).backward(dy)
         dx = Kn.conv2d_dgrad(dy.to(DEV), wd)
-        _close(dx, inp_r.grad, rtol=1e-4, atol=2e-5)
+        _close(dx, inp_r.grad, rtol=1e-4, atol=sc_(inp_r.grad))

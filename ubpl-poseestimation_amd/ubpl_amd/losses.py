@@ -67,6 +67,22 @@ def _f32c(t):
     return None if t is None else t.detach().float().contiguous()
 
 
+def _gate_rows(kpsGate, B, K, S):
+    """Gate per loss row.  With nStack == 1 and [B,1,...] predictions the
+    reference's rows are per sample (K == 1) while the gate is [B,Kg]:
+    `loss.mul(kpsGate)` broadcasts [B,1] x [B,Kg] (utils/losses.py:25), i.e.
+    each sample's loss is weighted by the SUM of its gates, and the count is
+    still #{gate > 0} over the full gate (:18-19).  Returns (gate rows, count
+    override or None)."""
+    gate = _f32c(kpsGate)
+    if gate is None or gate.shape[-1] == K:
+        return gate, None
+    if K != 1:
+        raise RuntimeError("kpsGate %s does not broadcast against %d rows per sample" % (tuple(gate.shape), K))
+    count = S * int((gate > 0).sum().item())
+    return gate.reshape(B, -1).sum(1, keepdim=True).contiguous(), count
+
+
 def _sw_vec(sw):
     return None if sw is None else sw.detach().float().reshape(-1).contiguous()
 
@@ -85,12 +101,12 @@ class JointMSELoss(nn.Module):
         t = gts.detach().contiguous()
         if t.numel() != B * K * HW:
             raise RuntimeError("gts do not match preds rows")
-        gate = _f32c(kpsGate)
+        gate, count = _gate_rows(kpsGate, B, K, S)
         sw = _sw_vec(sampleWeight) if self.useSampleWeight else None
         spec = (0, S, K, HW, (K * HW, 0, 0, 1), bool(self.useKPsGate and gate is not None),
                 bool(self.useSampleWeight and sw is not None), 0.0)
         s, cnt, _ = _RowLoss.apply(a, t, spec, gate, sw)
-        return s, int(cnt[0].item())
+        return s, count if count is not None else int(cnt[0].item())
 
 
 class JointDistLoss(nn.Module):
@@ -105,12 +121,12 @@ class JointDistLoss(nn.Module):
         a = preds1.contiguous()
         B, S, K, HW = _rows_of(a, self.nStack)
         t = preds2.contiguous()
-        gate = _f32c(kpsGate)
+        gate, count = _gate_rows(kpsGate, B, K, S)
         sw = _sw_vec(sampleWeight) if self.useSampleWeight else None
         spec = (0, S, K, HW, (S * K * HW, K * HW, 0, 1), bool(self.useKPsGate and gate is not None),
                 bool(self.useSampleWeight and sw is not None), 0.0)
         s, cnt, _ = _RowLoss.apply(a, t, spec, gate, sw)
-        return s, int(cnt[0].item())
+        return s, count if count is not None else int(cnt[0].item())
 
 
 class JointDistLoss_mt2(nn.Module):

@@ -1,0 +1,476 @@
+"""T1 — the training step of each project on the HIP path.
+
+Same signatures, batch formats and returned records as the reference
+train() functions (projects/MT_UBPL.py:157-352, projects/DualPose_UBPL.py:
+156-295, projects/MT.py:161-268, projects/supervised.py:135-175), so a
+project's epoch loop can call these instead.  What changes is where the work
+happens:
+
+* every loss sum AND every count stays on the device (the reference syncs
+  per element, ~8k host round trips per MT_UBPL step at B=32); the step makes
+  ONE device->host copy, at its end, for the records / the per-batch line;
+* heatmap targets can be rendered on the device inside the step (meta["kps"]
+  instead of rendered heatmaps), as the benchmark does;
+* the optimiser step and the EMA teacher update are single kernels over the
+  flat parameter buffers (FlatAdamW, update_ema_variables);
+* under torch.distributed every normaliser is global (one tiny all-reduce of
+  sums+counts after the forward) and the student gradients are SUM-reduced
+  once after the backward (ubpl_amd.dist).
+
+Reference semantics that look like bugs are kept: teachers run in train mode
+and keep their own BN statistics; EMA alpha is keyed on the epoch; the FDL
+term is added to both students' totals (its gradient applied twice); the
+pseudo-loss normaliser counts rows with a positive weighted loss.
+"""
+import torch
+
+from . import dist as D
+from . import kernels as Kn
+from .losses import AvgCounter, _RowLoss, features_cov
+from .parameters import update_ema_variables
+from .process import render_batch
+
+
+# ---------------------------------------------------------------------------
+# device-count loss helpers (same row semantics as ubpl_amd.losses)
+# ---------------------------------------------------------------------------
+def _mse(preds, gts, S, gate, sw):
+    """JointMSELoss(nStack=S, useKPsGate=True, useSampleWeight=True): (sum, cnt[4])."""
+    B, K = preds.shape[0], preds.shape[2]
+    HW = preds.shape[-1] * preds.shape[-2]
+    spec = (0, S, K, HW, (K * HW, 0, 0, 1), gate is not None, sw is not None, 0.0)
+    s, c, _ = _RowLoss.apply(preds, gts, spec, gate, sw)
+    return s, c
+
+
+def _mse_plain(preds, gts, S):
+    """JointMSELoss(nStack=S) without gate/weights (projects/supervised.py:138);
+    nStack == 1 keeps the reference's per-sample rows (reshape((bs, k, -1)))."""
+    B = preds.shape[0]
+    if S == 1:
+        K = preds.shape[1]
+        HW = preds.numel() // (B * K)
+        spec = (0, 1, K, HW, (K * HW, 0, 0, 1), False, False, 0.0)
+    else:
+        K = preds.shape[2]
+        HW = preds.shape[-1] * preds.shape[-2]
+        spec = (0, S, K, HW, (K * HW, 0, 0, 1), False, False, 0.0)
+    s, c, _ = _RowLoss.apply(preds, gts, spec, None, None)
+    return s, c
+
+
+def _dist_last(preds, tpreds):
+    """JointDistLoss() on the last stack of both (projects/MT_UBPL.py:250)."""
+    a = preds[:, -1].contiguous()
+    t = tpreds[:, -1].contiguous()
+    K = a.shape[1]
+    HW = a.shape[-1] * a.shape[-2]
+    spec = (0, 1, K, HW, (K * HW, K * HW, 0, 1), False, False, 0.0)
+    s, c, _ = _RowLoss.apply(a, t, spec, None, None)
+    return s, c
+
+
+def _dist_mt2_last(preds, tpreds, sw, thr):
+    """JointDistLoss_mt2(useSampleWeight=True, scoreThr) on the last stacks
+    (projects/DualPose_UBPL.py:163,203)."""
+    a = preds[:, -1].contiguous()
+    t = tpreds[:, -1].contiguous()
+    K = a.shape[1]
+    HW = a.shape[-1] * a.shape[-2]
+    spec = (1, 1, K, HW, (K * HW, K * HW, 0, 1), False, True, float(thr))
+    return _RowLoss.apply(a, t, spec, None, sw)
+
+
+def _pseudo(preds, targets, sw, S, thr):
+    """JointPseudoLoss3(nStack=S, scoreThr) with targets [M,B,S,K,R,R]."""
+    B, K = preds.shape[0], preds.shape[2]
+    HW = preds.shape[-1] * preds.shape[-2]
+    M, St = targets.shape[0], targets.shape[2]
+    spec = (2, S, K, HW, (St * K * HW, 0, B * St * K * HW, M, (St - 1) * K * HW), False, True, float(thr))
+    return _RowLoss.apply(preds, targets, spec, None, sw)
+
+
+def _norm(s, n):
+    """(s / n) if n > 0 else s — with n a device tensor."""
+    n = n.float()
+    return torch.where(n > 0, s / n.clamp(min=1.0), s)
+
+
+def _islabeled(meta_isl, dev):
+    return meta_isl.to(dev, non_blocking=True).reshape(-1)
+
+
+def _w(isl, lab, unlab):
+    one = torch.ones(isl.shape[0], device=isl.device)
+    return torch.where(isl > 0, lab * one, unlab * one).contiguous()
+
+
+def _targets(imgs, hms, meta, A, dev, args):
+    """Heatmaps and gates per view: either given (reference batch format) or
+    rendered on the device from meta['kps'] (list of [B,K,3] per view)."""
+    if hms is not None:
+        hs = [h[0].to(dev, non_blocking=True).float().contiguous() for h in hms]
+        gs = [kw[0].to(dev, non_blocking=True).float().contiguous() for kw in meta["kpsWeights"]]
+        return hs, gs
+    hs, gs = [], []
+    inp = imgs[0].shape[-1]
+    for a in range(A):
+        hm, kk = render_batch(meta["kps"][a].to(dev).float(), (imgs[a].shape[-2], imgs[a].shape[-1]), inp,
+                              args.outRes if hasattr(args, "outRes") else inp // 4)
+        hs.append(hm)
+        gs.append(kk[:, :, 2].contiguous())
+    return hs, gs
+
+
+def _sync_stats(local_sums, counts):
+    """One small all-reduce: returns (global counts, global sums) — identity
+    on one rank."""
+    if not D.is_dist():
+        return counts, local_sums
+    pack = torch.cat([counts.float(), local_sums.detach().float()])
+    D.allreduce_(pack)
+    n = counts.numel()
+    return pack[:n], pack[n:]
+
+
+# ---------------------------------------------------------------------------
+# MT_UBPL
+# ---------------------------------------------------------------------------
+def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
+    """projects/MT_UBPL.py:157-352 -> (pec_records, mtc_records, epc_records, fdc_record)."""
+    M = len(models)
+    pec_c = [AvgCounter() for _ in range(M)]
+    mtc_c = [AvgCounter() for _ in range(M)]
+    epc_c = [AvgCounter() for _ in range(M)]
+    fdc_c = AvgCounter()
+    dev = models[0].flat_params.device
+    S = args.nStack
+    for m in models:
+        m.train()
+    for e in models_ema:
+        e.train()
+    for bat, (augs_imgMap, augs_heatmaps, meta) in enumerate(trainLoader):
+        for o in optims:
+            o.zero_grad()
+        A = len(augs_imgMap)
+        imgs = [x.to(dev, non_blocking=True).float().contiguous() for x in augs_imgMap]
+        hms, gates = _targets(imgs, augs_heatmaps, meta, A, dev, args)
+        isl = _islabeled(meta["islabeled"][0], dev)
+        sw = _w(isl, 1.0, 0.0)                                   # getSampleWeight
+        nega = _w(isl, 0.0, args.pseudoWeight)                   # getSampleWeight_nega
+        B = imgs[0].shape[0]
+        outs, feats, outs_ema = [], [], []
+        for mi in range(M):                                      # :228-243
+            oa, fa, ea = [], [], []
+            for a in range(A):
+                o, f = models[mi](imgs[a])
+                oa.append(o)
+                fa.append(f)
+                with torch.no_grad():
+                    ea.append(models_ema[mi](imgs[a])[0])
+            outs.append(oa)
+            feats.append(fa)
+            outs_ema.append(ea)
+        K = outs[0][0].shape[2]
+        # ---- loss sums / counts on device
+        sums, cnts = [], []
+        ps_scores = []
+        for mi in range(M):
+            ms = []
+            for a in range(A):
+                s_d, _ = _dist_last(outs[mi][a], outs_ema[mi][a])
+                s_p, c_p = _mse(outs[mi][a], hms[a], S, gates[a], sw.reshape(-1, 1))
+                tg = torch.stack([outs_ema[j][a] for j in range(M)])
+                s_e, c_e, sc_e = _pseudo(outs[mi][a], tg, nega, S, args.pseudoScoreThr)
+                ms.append((s_d, s_p, c_p, s_e, c_e))
+                ps_scores.append(sc_e)
+            sums.append(ms)
+        fd = []
+        if args.FDLWeight > 0:
+            for a in range(A):                                   # :301-330 labeled rows
+                rowmask = _fdl_rows(sw, args)
+                v, c = features_cov(feats[0][a], feats[1][a], rowmask)
+                fd.append((v, c))
+        # pack: per model [mtc_sum, pec_sum, epc_sum], counts [pec_n, epc_n, n_sel] ; fdc
+        loc = []
+        cn = []
+        for mi in range(M):
+            loc += [sum(x[0] for x in sums[mi]), sum(x[1] for x in sums[mi]), sum(x[3] for x in sums[mi])]
+            cn += [sum(x[2][0] for x in sums[mi]), sum(x[4][1] for x in sums[mi]), sum(x[4][2] for x in sums[mi])]
+        if fd:
+            loc.append(sum(v for v, _ in fd))
+            cn.append(sum(c[0] for _, c in fd))
+        counts = torch.stack([c.float() for c in cn])
+        gcounts, gsums = _sync_stats(torch.stack([l.float() for l in loc]), counts)
+        W = D.world()
+        mtc_n = A * B * K * W
+        totals, rec = [], []
+        fdc = 0.
+        if fd:
+            fdc = args.FDLWeight * _norm(loc[-1], gcounts[-1])
+        for mi in range(M):
+            mtc = args.consWeight * (loc[3 * mi] / mtc_n)
+            pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[3 * mi])
+            epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[3 * mi + 1])
+            totals.append(pec + mtc + epc + fdc)
+            rec.append((pec, mtc, epc))
+        for t in totals:                                          # :334-336
+            t.backward(retain_graph=True)
+        D.allreduce_grads(models)
+        for o in optims:
+            o.step()
+        for mi, m in enumerate(models):
+            update_ema_variables(m, models_ema[mi], args)
+        # ---- records: one device->host copy
+        g_rec = []
+        for mi in range(M):
+            g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[3 * mi]),
+                      args.consWeight * gsums[3 * mi] / mtc_n,
+                      args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[3 * mi + 1])]
+        g_rec.append(args.FDLWeight * _norm(gsums[-1], gcounts[-1]) if fd else torch.zeros((), device=dev))
+        score = torch.stack(ps_scores).mean(0)
+        host = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, score]).cpu().tolist()
+        nrec = 3 * M + 1
+        for mi in range(M):
+            pec_c[mi].update(host[3 * mi], int(host[nrec + 3 * mi]))
+            mtc_c[mi].update(host[3 * mi + 1], mtc_n)
+            epc_c[mi].update(host[3 * mi + 2], int(host[nrec + 3 * mi + 1]))
+        if fd:
+            fdc_c.update(host[3 * M], int(host[nrec + 3 * M]))
+        else:
+            fdc_c.update(0., B)
+        if verbose:
+            n_ps = int(sum(host[nrec + 3 * mi + 1] for mi in range(M)))
+            n_sel = int(sum(host[nrec + 3 * mi + 2] for mi in range(M)))
+            sc = host[nrec + len(cn):]
+            print("batch.{} (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
+                format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
+                format(n_sel / n_ps if n_ps else float("nan"), ".2f"), format(n_sel, "5d"), format(n_ps, "5d"),
+                ", ".join(format(v, ".3f") for v in sc)))
+        del outs, outs_ema, feats, totals
+    return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
+
+
+def _fdl_rows(sw, args):
+    if args.FDL_label == "labeled":
+        return (sw > 0).float()
+    if args.FDL_label == "unlabeled":
+        return (sw == 0).float()
+    return torch.ones_like(sw)
+
+
+# ---------------------------------------------------------------------------
+# DualPose_UBPL
+# ---------------------------------------------------------------------------
+def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
+    """projects/DualPose_UBPL.py:156-295."""
+    M = len(models)
+    pec_c = [AvgCounter() for _ in range(M)]
+    mtc_c = [AvgCounter() for _ in range(M)]
+    epc_c = [AvgCounter() for _ in range(M)]
+    fdc_c = AvgCounter()
+    dev = models[0].flat_params.device
+    S = args.nStack
+    for m in models:
+        m.train()
+    for e in models_ema:
+        e.train()
+    for bat, (stu_imgMap, stu_heatmap, ema_imgMap, meta) in enumerate(trainLoader):
+        for o in optims:
+            o.zero_grad()
+        si = stu_imgMap.to(dev, non_blocking=True).float().contiguous()
+        ei = ema_imgMap.to(dev, non_blocking=True).float().contiguous()
+        if stu_heatmap is None:
+            hm, kk = render_batch(meta["kps"].to(dev).float(), (si.shape[-2], si.shape[-1]), si.shape[-1],
+                                  si.shape[-1] // 4)
+            gate = kk[:, :, 2].contiguous()
+        else:
+            hm = stu_heatmap.to(dev, non_blocking=True).float().contiguous()
+            gate = meta["kpsWeight"].to(dev, non_blocking=True).float().contiguous()
+        isl = _islabeled(meta["islabeled"], dev)
+        sw = _w(isl, 1.0, 0.0)
+        nega = _w(isl, 0.0, args.pseudoWeight)
+        cons = _w(isl, 1.0, args.pseudoWeight)
+        B = si.shape[0]
+        outs, feats = [], []
+        for mi in range(M):
+            o, f = models[mi](si)
+            outs.append(o)
+            feats.append(f)
+        with torch.no_grad():
+            outs_ema = torch.stack([models_ema[mi](ei)[0] for mi in range(M)])
+        loc, cn, cons_sc, ps_sc = [], [], [], []
+        for mi in range(M):
+            s_c, c_c, sc_c = _dist_mt2_last(outs[mi], outs_ema[mi], cons, args.pseudoScoreThr)
+            s_p, c_p = _mse(outs[mi], hm, S, gate, sw.reshape(-1, 1))
+            s_e, c_e, sc_e = _pseudo(outs[mi], outs_ema, nega, S, args.pseudoScoreThr)
+            loc += [s_c, s_p, s_e]
+            cn += [c_c[0], c_p[0], c_e[1], c_c[1], c_c[2], c_e[2]]
+            cons_sc.append(sc_c)
+            ps_sc.append(sc_e)
+        fd = None
+        if args.FDLWeight > 0:
+            fd = features_cov(feats[0], feats[1], _fdl_rows(sw, args))
+            loc.append(fd[0])
+            cn.append(fd[1][0])
+        counts = torch.stack([c.float() for c in cn])
+        gcounts, gsums = _sync_stats(torch.stack([l.float() for l in loc]), counts)
+        fdc = args.FDLWeight * _norm(fd[0], gcounts[-1]) if fd is not None else 0.
+        totals = []
+        for mi in range(M):
+            mtc = args.consWeight * _norm(loc[3 * mi], gcounts[6 * mi])
+            pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[6 * mi + 1])
+            epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2])
+            totals.append(pec + mtc + epc + fdc)
+        for t in totals:
+            t.backward(retain_graph=True)
+        D.allreduce_grads(models)
+        for o in optims:
+            o.step()
+        for mi, m in enumerate(models):
+            update_ema_variables(m, models_ema[mi], args)
+        g_rec = []
+        for mi in range(M):
+            g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[6 * mi + 1]),
+                      args.consWeight * _norm(gsums[3 * mi], gcounts[6 * mi]),
+                      args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[6 * mi + 2])]
+        g_rec.append(args.FDLWeight * _norm(gsums[-1], gcounts[-1]) if fd is not None else
+                     torch.zeros((), device=dev))
+        host = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, torch.stack(cons_sc).mean(0),
+                          torch.stack(ps_sc).mean(0)]).cpu().tolist()
+        nrec = 3 * M + 1
+        cbase = nrec
+        for mi in range(M):
+            pec_c[mi].update(host[3 * mi], int(host[cbase + 6 * mi + 1]))
+            mtc_c[mi].update(host[3 * mi + 1], int(host[cbase + 6 * mi]))
+            epc_c[mi].update(host[3 * mi + 2], int(host[cbase + 6 * mi + 2]))
+        if fd is not None:
+            fdc_c.update(host[3 * M], int(host[cbase + 6 * M]))
+        else:
+            fdc_c.update(0., B)
+        if verbose:
+            K = outs[0].shape[2]
+            off = cbase + len(cn)
+            c_ps = int(sum(host[cbase + 6 * mi + 3] for mi in range(M)))
+            c_sel = int(sum(host[cbase + 6 * mi + 4] for mi in range(M)))
+            e_ps = int(sum(host[cbase + 6 * mi + 2] for mi in range(M)))
+            e_sel = int(sum(host[cbase + 6 * mi + 5] for mi in range(M)))
+            print("batch.{} consist-pseudo (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
+                format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
+                format(c_sel / c_ps if c_ps else float("nan"), ".2f"), format(c_sel, "5d"), format(c_ps, "5d"),
+                ", ".join(format(v, ".3f") for v in host[off:off + K])))
+            print("batch.{} ensemble-pseudo (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
+                format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
+                format(e_sel / e_ps if e_ps else float("nan"), ".2f"), format(e_sel, "5d"), format(e_ps, "5d"),
+                ", ".join(format(v, ".3f") for v in host[off + K:off + 2 * K])))
+        del outs, outs_ema, feats, totals
+    return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
+
+
+# ---------------------------------------------------------------------------
+# MT and supervised
+# ---------------------------------------------------------------------------
+def train_mt(trainLoader, model, model_ema, optim, args):
+    """projects/MT.py:161-268 -> (pec_avg, mtc_avg)."""
+    pec_c, mtc_c = AvgCounter(), AvgCounter()
+    dev = model.flat_params.device
+    S = args.nStack
+    model.train()
+    model_ema.train()
+    pick = (lambda r: r) if args.feature_mode == "default" else (lambda r: r[0])
+    for bat, (augs_imgMap, augs_heatmaps, meta) in enumerate(trainLoader):
+        optim.zero_grad()
+        A = len(augs_imgMap)
+        imgs = [x.to(dev, non_blocking=True).float().contiguous() for x in augs_imgMap]
+        hms, gates = _targets(imgs, augs_heatmaps, meta, A, dev, args)
+        sw = _w(_islabeled(meta["islabeled"][0], dev), 1.0, 0.0)
+        outs, outs_ema = [], []
+        for a in range(A):
+            outs.append(pick(model(imgs[a])))
+            with torch.no_grad():
+                outs_ema.append(pick(model_ema(imgs[a])))
+        B, K = outs[0].shape[0], outs[0].shape[2]
+        sd = sum(_dist_last(outs[a], outs_ema[a])[0] for a in range(A))
+        ps = [_mse(outs[a], hms[a], S, gates[a], sw.reshape(-1, 1)) for a in range(A)]
+        sp = sum(p[0] for p in ps)
+        cp = sum(p[1][0] for p in ps)
+        counts, sums = _sync_stats(torch.stack([sd, sp]), cp.float().reshape(1))
+        mtc_n = A * B * K * D.world()
+        mtc = args.consWeight * (sd / mtc_n)
+        pec = args.poseWeight * _norm(sp, counts[0])
+        (pec + mtc).backward()
+        D.allreduce_grads([model])
+        optim.step()
+        update_ema_variables(model, model_ema, args)
+        host = torch.stack([args.poseWeight * _norm(sums[1], counts[0]), args.consWeight * sums[0] / mtc_n,
+                            counts[0]]).cpu().tolist()
+        mtc_c.update(host[1], mtc_n)
+        pec_c.update(host[0], int(host[2]))
+    return pec_c.avg, mtc_c.avg
+
+
+def train_supervised(trainLoader, model, optim, args):
+    """projects/supervised.py:135-175 -> pec_avg."""
+    pec_c = AvgCounter()
+    dev = model.flat_params.device
+    model.train()
+    pick = (lambda r: r) if args.feature_mode == "default" else (lambda r: r[0])
+    for bat, (imgMap, heatmap, meta) in enumerate(trainLoader):
+        optim.zero_grad()
+        img = imgMap.to(dev, non_blocking=True).float().contiguous()
+        hm = heatmap.to(dev, non_blocking=True).float().contiguous()
+        out = pick(model(img))
+        s, c = _mse_plain(out, hm, args.nStack)
+        counts, sums = _sync_stats(s.reshape(1), c[0].float().reshape(1))
+        pec = args.poseWeight * _norm(s, counts[0])
+        pec.backward()
+        D.allreduce_grads([model])
+        optim.step()
+        host = torch.stack([args.poseWeight * _norm(sums[0], counts[0]), counts[0]]).cpu().tolist()
+        pec_c.update(host[0], int(host[1]))
+    return pec_c.avg
+
+
+# ---------------------------------------------------------------------------
+# validate: teachers in eval mode -> decode -> PCK (D1-D5)
+# ---------------------------------------------------------------------------
+def validate(validLoader, models_ema, args):
+    """projects/MT_UBPL.py:355-408 -> (predsArray, accs_records, errs_records);
+    entries per teacher plus their mean (brNum + 1)."""
+    from .evaluation import EvaluationUtils
+    from .losses import AvgCounters
+    from .process import inverse_transforms
+    n = len(models_ema) + 1
+    accs_c = [AvgCounters() for _ in range(n)]
+    errs_c = [AvgCounters() for _ in range(n)]
+    preds_arr = [[] for _ in range(n)]
+    for e in models_ema:
+        e.eval()
+    dev = models_ema[0].flat_params.device
+    with torch.no_grad():
+        for bat, (imgMap, heatmap, meta) in enumerate(validLoader):
+            img = imgMap.to(dev, non_blocking=True).float().contiguous()
+            bs, k = heatmap.shape[0], heatmap.shape[1]
+            tinv = inverse_transforms(meta["center"], meta["scale"], [args.outRes, args.outRes]).to(dev)
+            pm = []
+            for e in models_ema:
+                o = e(img)
+                o = o[0] if isinstance(o, tuple) else o
+                _, p, _ = Kn.decode_heatmaps(o[:, -1].contiguous(), tinv)
+                pm.append(p)
+            pm.append(torch.stack(pm, -1).mean(-1))
+            gts = meta["kpsMap"].to(dev).float().contiguous()
+            outs = [EvaluationUtils.acc_pck(p, gts, args.pck_ref, args.pck_thr) for p in pm]
+            host = torch.cat([torch.cat([er, ac]) for er, ac in outs] + [p.reshape(-1) for p in pm]).cpu()
+            for mi in range(n):
+                errs = host[mi * 2 * (k + 1):mi * 2 * (k + 1) + k + 1]
+                accs = host[mi * 2 * (k + 1) + k + 1:(mi + 1) * 2 * (k + 1)]
+                for idx in range(k + 1):
+                    accs_c[mi].update(idx, accs[idx].item(), bs if idx < k else bs * k)
+                    errs_c[mi].update(idx, errs[idx].item(), bs if idx < k else bs * k)
+            base = n * 2 * (k + 1)
+            for mi in range(n):
+                preds_arr[mi] += host[base + mi * bs * k * 2:base + (mi + 1) * bs * k * 2].reshape(bs, k, 2).tolist()
+    for e in models_ema:
+        e.train()
+    return preds_arr, [c.avg() for c in accs_c], [c.avg() for c in errs_c]
