@@ -327,7 +327,7 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(case):
     yd = Kn.conv2d_forward(xd, wd, bd, st, scd, shd, res=res.to(DEV) if resid else None)
     # exact-f32 MFMA chains vs MKL: elementwise within 1e-4 relative, or 1e-5 of
     # the tensor's scale for elements near a cancellation to ~0
-    sc_ = lambda t: 1e-5 * float(t.abs().max())
+    sc_ = lambda t: 1e-5 * float(t.detach().abs().max())
     _close(yd, yref, rtol=1e-4, atol=sc_(yref))
     dw, db = torch.zeros_like(wd), torch.zeros_like(bd)
     Kn.conv2d_wgrad(dy.to(DEV), xd, KS, st, dw, db, scd, shd, accumulate=True)

@@ -322,8 +322,9 @@ class _HourglassFn(torch.autograd.Function):
             model.attach_grad_views()
         if dfeats is not None and dfeats.numel() == 0:
             dfeats = None
+        # the saved activations stay with ctx: the reference runs backward(retain_graph=True)
+        # once per student and the shared FDL term reaches both networks twice
         model._backward_impl(ctx.ex, dpreds, dfeats)
-        ctx.ex = None
         return None, None, None
 
 
