@@ -9,8 +9,8 @@ the reference's own train() on the same inputs).  Checked:
   agree with the oracle's step (run here on the CPU) on >= 97 % of each
   student's weights and >= 90 % of every tensor (grads whose sign is below fp32 noise can flip — the
   reference's own fp32 gradients are ~2 % from exact, see test_gpu_hourglass);
-* teachers after the EMA update: 5e-3 relative per tensor (they average in
-  the students' sign-flipped updates);
+* teachers after the EMA update equal alpha*teacher + (1-alpha)*student
+  (alpha keyed on the epoch) to fp32 rounding;
 * BN running statistics: 1e-3 relative.
 """
 import os
@@ -108,8 +108,12 @@ def test_train_step_vs_reference(case, flat_adam):
                 agree_n, total_n = agree_n + same, total_n + du.numel()
                 assert same >= 0.9 * du.numel(), (mi, n, same / du.numel())
             else:
-                err = float((p.detach().cpu().double() - q.detach().double()).norm() / (q.double().norm() + 1e-30))
-                assert err < 5e-3 or seeds.bn_cancelled(n), (mi, n, err)
+                # teacher = alpha*teacher + (1-alpha)*student_after_step (utils/parameters.py:6-8),
+                # checked on our own tensors (the students were checked against the oracle above)
+                s_new = dict(ours[mi - len(ours) // 2].named_parameters())[n].detach().cpu()
+                alpha = min(1 - 1 / (args.epo + 1), args.ema_decay)
+                expect = p0.cpu() * alpha + (1 - alpha) * s_new
+                assert torch.allclose(p.detach().cpu(), expect, rtol=2e-7, atol=1e-9), (mi, n)
         if mi < n_students:
             assert agree_n >= 0.97 * total_n, (mi, agree_n / total_n)
         for (bn, b), (_, rb) in zip(m.named_buffers(), r.named_buffers()):
