@@ -81,12 +81,12 @@ class ConvTimer:
     def __enter__(self):
         orig = self.orig
 
-        def wrapped(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out=None):
-            if not self.active or w.shape[-1] != 3 or pscale is None:
-                return orig(x, w, bias, stride, pscale, pshift, res, out)
+        def wrapped(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out=None, w_tap=None):
+            if not self.active or w is None or w.shape[-1] != 3 or pscale is None:
+                return orig(x, w, bias, stride, pscale, pshift, res, out, w_tap)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            y = orig(x, w, bias, stride, pscale, pshift, res, out)
+            y = orig(x, w, bias, stride, pscale, pshift, res, out, w_tap)
             e.record()
             self.events.append((s, e))
             B, Cin = x.shape[:2]

@@ -101,14 +101,22 @@ int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, cons
 
 /* Conv (models/base/layers.py:31-50): 1x1/s1, 3x3/s1, 7x7/s2, pad (KS-1)/2,
  * optional fused pre-activation relu(x*pscale + pshift), bias, residual add
- * (res may alias y).  MFMA f32 implicit GEMM. */
+ * (res may alias y).  MFMA f32 implicit GEMM, tap-major K (k = tap*Cin + ci):
+ * for KS > 1 the weights must be in the layout ubpl_conv_weight_tapmajor makes.
+ * Small grids split K over workgroups: slab = ubpl_conv2d_forward_workspace
+ * floats (nullable when that is 0). */
+int64_t ubpl_conv2d_forward_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo);
 int ubpl_conv2d_forward(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias, int Cout,
                         int KS, int stride, const float* pscale, const float* pshift, const float* res, float* y,
-                        int Ho, int Wo, void* stream);
+                        int Ho, int Wo, float* slab, void* stream);
+int ubpl_conv_weight_tapmajor(const float* w, int Cout, int Cin, int KS, float* wt, void* stream);
+/* Weight gradient (+ bias gradient), reference weight layout. */
 int64_t ubpl_conv2d_wgrad_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo);
 int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, int H, int W, int Cout, int KS, int stride,
                       const float* pscale, const float* pshift, int Ho, int Wo, float* slab, float* dw, float* db,
                       int accumulate, void* stream);
+/* Data-gradient weights (stride 1): the tap-major layout of the flipped,
+ * transposed kernel, so dx = ubpl_conv2d_forward(dy, wt). */
 int ubpl_conv_weight_flip(const float* w, int Cout, int Cin, int KS, float* wt, void* stream);
 
 /* MaxPool2d(2,2) (models/base/layers.py:93), Upsample(x2, nearest) + add

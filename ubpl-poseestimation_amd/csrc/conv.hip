@@ -5,22 +5,28 @@
 // (models/pose/hourglass.py:22).
 //
 // GEMM view, NCHW, n = b*P + p (P = Ho*Wo, contiguous in memory):
-//   forward  Y[b,m,p] = sum_k W[m,k] * X~[b,k,p] + bias[m] (+ R[b,m,p])
-//            k = ci*KS*KS + kh*KS + kw, X~ = im2col of relu(x*scale + shift)
-//            (the pre-activation BN+ReLU of Residual is applied while the
-//            operand is staged: bn(x) is never written to HBM);
-//   dgrad    = forward with the weights transposed/flipped (stride 1 only);
-//   wgrad    dW[m,n] = sum_k dY[m,k] * X~[k,n] over k = (b, p), split over
-//            workgroups along k into a slab, reduced deterministically; the
-//            n-tile-0 workgroups also sum dY rows -> the bias gradient.
+//   forward  Y[b,m,p] = sum_k W~[m,k] * X~[b,k,p] + bias[m] (+ R[b,m,p])
+//            TAP-MAJOR k = tap*Cin + ci (tap = kh*KS + kw), W~ = the weights
+//            re-laid out [Cout][KS*KS][Cin] (ubpl_conv_weight_tapmajor), so a
+//            K tile of BK channels shares one tap: each thread derives its
+//            input coordinates once per tile, not per element.  X~ = im2col of
+//            relu(x*scale + shift): the pre-activation BN+ReLU of Residual is
+//            applied while the operand is staged (bn(x) never touches HBM;
+//            scale/shift sit in LDS for the whole workgroup);
+//   dgrad    = forward with the weights flipped/transposed (stride 1 only);
+//   wgrad    dW[m,n] = sum_k dY[m,k] * X~[k,n] over k = (b, p), n tap-major,
+//            split along k over workgroups into a slab and reduced
+//            deterministically (the reduce writes the reference layout);
+//            the n-tile-0 workgroups also sum dY rows = the bias gradient.
+// Small grids (deep hourglass levels: 32x32 .. 4x4 planes, K = 1152) split K
+// over workgroups too (slab + reduce-epilogue), so every level fills the chip.
 //
-// Matrix core: v_mfma_f32_32x32x2_f32 (exact f32 fmaf chains, the fp32 path
-// the parity tests hold to 1e-4).  Lane maps (cdna_hip_programming.md §3):
-// A[i=l&31][k=l>>5], B[k=l>>5][j=l&31], C/D col = l&31,
-// row = (r&3) + 8*(r>>2) + 4*(l>>5).  Block = 4 waves in a 2x2 grid; both
-// operands staged k-major in LDS (As[k][m], Bs[k][n]) so a wave's fragment
-// read is 32 consecutive floats per half-wave; register-staged double buffer
-// (global loads of tile t+1 issued before the MFMAs of tile t).
+// Matrix core: v_mfma_f32_32x32x2_f32 (exact f32 fmaf chains).  Lane maps
+// (cdna_hip_programming.md §3): A[i=l&31][k=l>>5], B[k=l>>5][j=l&31],
+// C/D col = l&31, row = (r&3) + 8*(r>>2) + 4*(l>>5).  4 waves in a 2x2 grid;
+// operands staged k-major in LDS (As[k][m], Bs[k][n]) so a fragment read is
+// 32 consecutive floats per half-wave; register-staged double buffer with one
+// barrier per K step.
 #include "common.h"
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -28,107 +34,138 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 namespace {
 
 constexpr int NT = 256;
+constexpr int BK = 16;
+constexpr int MAXC = 256;  // largest Cin with a fused BN prologue
 
 // ------------------------------------------------------------------ forward
-template <int BM, int BN, int BK, int KS, int ST, bool PRO, bool VECB>
-struct FwdCfg {
-    static constexpr int PADK = (KS - 1) / 2;
-    static constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 MFMA tiles per wave
-    static constexpr int ALD = BM + 2, BLD = BN + 4;  // LDS row lengths (floats)
-    static constexpr int A_PER = BM * BK / NT, B_PER = BK * BN / NT;
-};
-
-template <int BM, int BN, int BK, int KS, int ST, bool PRO, bool VECB>
+// TAPK: k tiles never straddle a tap (Cin % BK == 0 or KS == 1).
+template <int BM, int BN, int KS, int ST, bool PRO, bool VECB, bool TAPK>
 __global__ void __launch_bounds__(NT) conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ bias,
                                                      const float* __restrict__ pscale,
-                                                     const float* __restrict__ pshift, const float* res,
-                                                     float* y, int B, int Cin, int H, int W, int Cout, int Ho,
-                                                     int Wo) {
-    using C = FwdCfg<BM, BN, BK, KS, ST, PRO, VECB>;
-    __shared__ float As[2][BK][C::ALD];
-    __shared__ float Bs[2][BK][C::BLD];
+                                                     const float* __restrict__ pshift, const float* res, float* y,
+                                                     int B, int Cin, int H, int W, int Cout, int Ho, int Wo,
+                                                     int kchunk, float* __restrict__ slab) {
+    constexpr int PADK = (KS - 1) / 2;
+    constexpr int TM = BM / 64, TN = BN / 64;
+    constexpr int ALD = BM + 2, BLD = BN + 4;
+    constexpr int A_PER = BM * BK / NT;          // 8 (BM=128) or 4 (BM=64)
+    constexpr int B_PER = BK * BN / NT;          // 8
+    constexpr int VROWS = NT / (BN / 4);         // vector loader rows per pass
+    __shared__ float As[2][BK][ALD];
+    __shared__ float Bs[2][BK][BLD];
+    __shared__ float s_sc[PRO ? MAXC : 1], s_sh[PRO ? MAXC : 1];
 
-    const int P = Ho * Wo;
+    const int P = Ho * Wo, HWin = H * W;
     const int64_t N = (int64_t)B * P;
     const int Ktot = Cin * KS * KS;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
     const int m0 = blockIdx.y * BM;
     const int64_t n0 = (int64_t)blockIdx.x * BN;
+    const int k_begin = blockIdx.z * kchunk;
+    const int k_end = min(Ktot, k_begin + kchunk);
 
-    // ---- A loader: thread owns row am, k chunk ak0 .. ak0+A_PER-1
-    const int am = tid % BM;
-    const int ak0 = (tid / BM) * C::A_PER;
-    // ---- B loader (scalar): thread owns column bnl, rows bk0 + j*(NT/BN)
-    const int bnl = tid % BN;
-    const int bk0 = tid / BN;
-    // ---- B loader (vector 1x1): thread owns 4 columns 4*(tid % (BN/4)), rows
-    const int vn4 = tid % (BN / 4);
-    const int vk0 = tid / (BN / 4);
-    constexpr int VROWS = NT / (BN / 4);  // rows covered per pass
-
-    // Column decomposition for the scalar loader (fixed per thread per tile)
-    int cb = 0, coh = 0, cow = 0;
-    bool cvalid;
-    {
-        const int64_t n = n0 + (VECB ? 4 * vn4 : bnl);
-        cvalid = n < N;
-        if (cvalid) {
-            cb = (int)(n / P);
-            const int p = (int)(n - (int64_t)cb * P);
-            coh = p / Wo;
-            cow = p - coh * Wo;
+    if (PRO) {
+        for (int c = tid; c < Cin; c += NT) {
+            s_sc[c] = pscale[c];
+            s_sh[c] = pshift[c];
         }
     }
 
-    float ra[C::A_PER];
-    float rb[VECB ? 4 * (BK / VROWS) : C::B_PER];
+    // A loader: row am, k chunk ak0 .. ak0 + A_PER - 1 (vectorised when aligned)
+    const int am = tid % BM;
+    const int ak0 = (tid / BM) * A_PER;
+    const bool avec = (Ktot % 4) == 0;
+    // B loader column(s)
+    const int bnl = VECB ? 4 * (tid % (BN / 4)) : tid % BN;
+    const int bk0 = VECB ? tid / (BN / 4) : tid / BN;
+    int cb = 0, coh = 0, cow = 0;
+    const int64_t ncol = n0 + bnl;
+    const bool cvalid = ncol < N;
+    if (cvalid) {
+        cb = (int)(ncol / P);
+        const int p = (int)(ncol - (int64_t)cb * P);
+        coh = p / Wo;
+        cow = p - coh * Wo;
+    }
+    const float* xb = x + (int64_t)cb * Cin * HWin;
+
+    float ra[A_PER];
+    float rb[B_PER];
 
     auto load_a = [&](int kt) {
+        const int m = m0 + am;
+        const int k = kt + ak0;
+        if (m < Cout && avec && k + A_PER <= k_end) {
+            const float4* src = reinterpret_cast<const float4*>(w + (int64_t)m * Ktot + k);
 #pragma unroll
-        for (int j = 0; j < C::A_PER; ++j) {
-            const int k = kt + ak0 + j;
-            const int m = m0 + am;
-            ra[j] = (m < Cout && k < Ktot) ? w[(int64_t)m * Ktot + k] : 0.f;
+            for (int j = 0; j < A_PER / 4; ++j) {
+                const float4 v = src[j];
+                ra[4 * j] = v.x;
+                ra[4 * j + 1] = v.y;
+                ra[4 * j + 2] = v.z;
+                ra[4 * j + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < A_PER; ++j)
+                ra[j] = (m < Cout && k + j < k_end) ? w[(int64_t)m * Ktot + k + j] : 0.f;
         }
     };
     auto load_b = [&](int kt) {
         if constexpr (VECB) {
-            // 1x1 stride 1: X~[k][n..n+3] = x[b, k, p..p+3] (P % 4 == 0)
+            // 1x1 stride 1: X~[ci][n..n+3] = x[b, ci, p..p+3] (P % 4 == 0)
+            const int p = coh * Wo + cow;
 #pragma unroll
             for (int j = 0; j < BK / VROWS; ++j) {
-                const int k = kt + vk0 + j * VROWS;
+                const int k = kt + bk0 + j * VROWS;
                 float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (cvalid && k < Ktot) {
-                    const int p = coh * Wo + cow;
-                    v = *reinterpret_cast<const float4*>(x + ((int64_t)cb * Cin + k) * P + p);
+                if (cvalid && k < k_end) {
+                    v = *reinterpret_cast<const float4*>(xb + (int64_t)k * P + p);
                     if (PRO) {
-                        const float sc = pscale[k], sh = pshift[k];
+                        const float sc = s_sc[k], sh = s_sh[k];
                         v.x = fmaxf(fmaf(v.x, sc, sh), 0.f);
                         v.y = fmaxf(fmaf(v.y, sc, sh), 0.f);
                         v.z = fmaxf(fmaf(v.z, sc, sh), 0.f);
                         v.w = fmaxf(fmaf(v.w, sc, sh), 0.f);
                     }
                 }
-                rb[4 * j + 0] = v.x;
+                rb[4 * j] = v.x;
                 rb[4 * j + 1] = v.y;
                 rb[4 * j + 2] = v.z;
                 rb[4 * j + 3] = v.w;
             }
-        } else {
+        } else if constexpr (TAPK) {
+            // one tap for the whole K tile: input coordinates once per tile
+            const int tap = kt / Cin, ci0 = kt - tap * Cin;
+            const int kh = tap / KS, kw = tap - kh * KS;
+            const int ih = coh * ST - PADK + kh, iw = cow * ST - PADK + kw;
+            const bool inb = cvalid && ih >= 0 && ih < H && iw >= 0 && iw < W;
+            const float* src = xb + (int64_t)ci0 * HWin + (inb ? ih * W + iw : 0);
 #pragma unroll
-            for (int j = 0; j < C::B_PER; ++j) {
+            for (int j = 0; j < B_PER; ++j) {
+                const int r = bk0 + j * (NT / BN);
+                float v = 0.f;
+                if (inb && kt + r < k_end) {
+                    v = src[(int64_t)r * HWin];
+                    if (PRO) v = fmaxf(fmaf(v, s_sc[ci0 + r], s_sh[ci0 + r]), 0.f);
+                }
+                rb[j] = v;
+            }
+        } else {
+            // generic (stem, Cin = 3): tap and channel per element
+#pragma unroll
+            for (int j = 0; j < B_PER; ++j) {
                 const int k = kt + bk0 + j * (NT / BN);
                 float v = 0.f;
-                if (cvalid && k < Ktot) {
-                    const int ci = k / (KS * KS);
-                    const int r = k - ci * (KS * KS);
-                    const int kh = r / KS, kw = r - kh * KS;
-                    const int ih = coh * ST - C::PADK + kh, iw = cow * ST - C::PADK + kw;
+                if (cvalid && k < k_end) {
+                    const int tap = k / Cin, ci = k - tap * Cin;
+                    const int kh = tap / KS, kw = tap - kh * KS;
+                    const int ih = coh * ST - PADK + kh, iw = cow * ST - PADK + kw;
                     if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
-                        v = x[(((int64_t)cb * Cin + ci) * H + ih) * W + iw];
-                        if (PRO) v = fmaxf(fmaf(v, pscale[ci], pshift[ci]), 0.f);
+                        v = xb[(int64_t)ci * HWin + ih * W + iw];
+                        if (PRO) v = fmaxf(fmaf(v, s_sc[ci], s_sh[ci]), 0.f);
                     }
                 }
                 rb[j] = v;
@@ -137,49 +174,52 @@ __global__ void __launch_bounds__(NT) conv_fwd_kernel(const float* __restrict__ 
     };
     auto store_ab = [&](int buf) {
 #pragma unroll
-        for (int j = 0; j < C::A_PER; ++j) As[buf][ak0 + j][am] = ra[j];
+        for (int j = 0; j < A_PER; ++j) As[buf][ak0 + j][am] = ra[j];
         if constexpr (VECB) {
 #pragma unroll
             for (int j = 0; j < BK / VROWS; ++j)
-                *reinterpret_cast<float4*>(&Bs[buf][vk0 + j * VROWS][4 * vn4]) =
+                *reinterpret_cast<float4*>(&Bs[buf][bk0 + j * VROWS][bnl]) =
                     make_float4(rb[4 * j], rb[4 * j + 1], rb[4 * j + 2], rb[4 * j + 3]);
         } else {
 #pragma unroll
-            for (int j = 0; j < C::B_PER; ++j) Bs[buf][bk0 + j * (NT / BN)][bnl] = rb[j];
+            for (int j = 0; j < B_PER; ++j) Bs[buf][bk0 + j * (NT / BN)][bnl] = rb[j];
         }
     };
 
-    floatx16 acc[C::TM][C::TN];
+    floatx16 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < C::TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < C::TN; ++j)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const int nkt = (Ktot + BK - 1) / BK;
-    load_a(0);
-    load_b(0);
-    store_ab(0);
+    if (PRO) __syncthreads();  // s_sc / s_sh ready
+    const int nkt = (k_end - k_begin + BK - 1) / BK;
+    if (nkt > 0) {
+        load_a(k_begin);
+        load_b(k_begin);
+        store_ab(0);
+    }
     __syncthreads();
     const int li = lane & 31, lk = lane >> 5;
     for (int t = 0; t < nkt; ++t) {
         const int cur = t & 1;
         if (t + 1 < nkt) {
-            load_a((t + 1) * BK);
-            load_b((t + 1) * BK);
+            load_a(k_begin + (t + 1) * BK);
+            load_b(k_begin + (t + 1) * BK);
         }
 #pragma unroll
         for (int s = 0; s < BK / 2; ++s) {
-            float af[C::TM], bf[C::TN];
+            float af[TM], bf[TN];
 #pragma unroll
-            for (int i = 0; i < C::TM; ++i) af[i] = As[cur][2 * s + lk][wm + 32 * i + li];
+            for (int i = 0; i < TM; ++i) af[i] = As[cur][2 * s + lk][wm + 32 * i + li];
 #pragma unroll
-            for (int j = 0; j < C::TN; ++j) bf[j] = Bs[cur][2 * s + lk][wn + 32 * j + li];
+            for (int j = 0; j < TN; ++j) bf[j] = Bs[cur][2 * s + lk][wn + 32 * j + li];
 #pragma unroll
-            for (int i = 0; i < C::TM; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < C::TN; ++j)
+                for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
         }
         if (t + 1 < nkt) {
@@ -188,15 +228,32 @@ __global__ void __launch_bounds__(NT) conv_fwd_kernel(const float* __restrict__ 
         }
     }
 
+    if (slab != nullptr) {
+        // split-K partial tile: slab[z][m][n]
+        float* sl = slab + (int64_t)blockIdx.z * Cout * N;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int64_t n = n0 + wn + 32 * j + li;
+            if (n >= N) continue;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+                    if (m < Cout) sl[(int64_t)m * N + n] = acc[i][j][r];
+                }
+        }
+        return;
+    }
     // ---- epilogue: + bias (+ residual), coalesced along n
 #pragma unroll
-    for (int j = 0; j < C::TN; ++j) {
+    for (int j = 0; j < TN; ++j) {
         const int64_t n = n0 + wn + 32 * j + li;
         if (n >= N) continue;
         const int b = (int)(n / P);
         const int p = (int)(n - (int64_t)b * P);
 #pragma unroll
-        for (int i = 0; i < C::TM; ++i) {
+        for (int i = 0; i < TM; ++i) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
@@ -212,8 +269,29 @@ __global__ void __launch_bounds__(NT) conv_fwd_kernel(const float* __restrict__ 
     }
 }
 
+// y[b,m,p] = sum_z slab[z][m][b*P+p] + bias[m] (+ res)
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int splits, int Cout,
+                                                           int P, int64_t N, const float* __restrict__ bias,
+                                                           const float* res, float* y) {
+    const int64_t total = (int64_t)Cout * N;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        // i enumerates the output in NCHW order: i = (b*Cout + m)*P + p
+        const int p = (int)(i % P);
+        const int64_t t = i / P;
+        const int m = (int)(t % Cout);
+        const int64_t b = t / Cout;
+        const int64_t n = b * P + p;
+        float s = 0.f;
+        for (int z = 0; z < splits; ++z) s += slab[((int64_t)z * Cout + m) * N + n];
+        if (bias) s += bias[m];
+        if (res) s += res[i];
+        y[i] = s;
+    }
+}
+
 // ------------------------------------------------------------------ wgrad
-template <int BM, int BN, int BK, int KS, int ST, bool PRO>
+// n tap-major: n = tap*Cin + ci; TAPN: a BN-wide n tile lies in one tap.
+template <int BM, int BN, int KS, int ST, bool PRO, bool TAPN>
 __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                        const float* __restrict__ pscale,
                                                        const float* __restrict__ pshift, int B, int Cin, int H,
@@ -221,15 +299,15 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
                                                        float* __restrict__ slab, int with_bias) {
     constexpr int PADK = (KS - 1) / 2;
     constexpr int TM = BM / 64, TN = BN / 64;
+    constexpr int WBK = 32;
     constexpr int ALD = BM + 1, BLD = BN + 1;
-    constexpr int KL = 32;                 // lanes along k in the loaders
-    constexpr int RSTEP = NT / KL;         // rows per loader pass
+    constexpr int RSTEP = NT / WBK;
     constexpr int A_PER = BM / RSTEP, B_PER = BN / RSTEP;
-    static_assert(BK == KL, "loader assumes BK == 32");
-    __shared__ float As[2][BK][ALD];
-    __shared__ float Bs[2][BK][BLD];
+    __shared__ float As[2][WBK][ALD];
+    __shared__ float Bs[2][WBK][BLD];
+    __shared__ float s_sc[PRO ? MAXC : 1], s_sh[PRO ? MAXC : 1];
 
-    const int P = Ho * Wo;
+    const int P = Ho * Wo, HWin = H * W;
     const int64_t Kall = (int64_t)B * P;
     const int Ntot = Cin * KS * KS;
     const int Nt = Ntot + 1;
@@ -239,10 +317,20 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
     const int nb0 = blockIdx.x * BN;
     const int64_t k_begin = (int64_t)blockIdx.z * kchunk;
     const int64_t k_end = min(Kall, k_begin + kchunk);
-
-    const int lk_ld = tid % KL;    // loader: k within tile
-    const int lr_ld = tid / KL;    // loader: first row
+    const int lk_ld = tid % WBK;
+    const int lr_ld = tid / WBK;
     const bool bias_blk = with_bias && blockIdx.x == 0;
+    // tap of this workgroup's n tile (TAPN)
+    const int tap_blk = nb0 / Cin, ci_blk = nb0 - tap_blk * Cin;
+    const int kh_blk = tap_blk / KS, kw_blk = tap_blk - kh_blk * KS;
+
+    if (PRO) {
+        for (int c = tid; c < Cin; c += NT) {
+            s_sc[c] = pscale[c];
+            s_sh[c] = pshift[c];
+        }
+        __syncthreads();
+    }
 
     float ra[A_PER], rb[B_PER];
     auto load = [&](int64_t kt) {
@@ -260,21 +348,38 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
             const int m = m0 + lr_ld + j * RSTEP;
             ra[j] = (kv && m < Cout) ? dy[((int64_t)b * Cout + m) * P + p] : 0.f;
         }
+        const float* xb = x + (int64_t)b * Cin * HWin;
+        if constexpr (TAPN) {
+            const int ih = oh * ST - PADK + kh_blk, iw = ow * ST - PADK + kw_blk;
+            const bool inb = kv && ih >= 0 && ih < H && iw >= 0 && iw < W;
+            const float* src = xb + (inb ? ih * W + iw : 0);
 #pragma unroll
-        for (int j = 0; j < B_PER; ++j) {
-            const int n = nb0 + lr_ld + j * RSTEP;
-            float v = 0.f;
-            if (kv && n < Ntot) {
-                const int ci = n / (KS * KS);
-                const int r = n - ci * (KS * KS);
-                const int kh = r / KS, kw = r - kh * KS;
-                const int ih = oh * ST - PADK + kh, iw = ow * ST - PADK + kw;
-                if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
-                    v = x[(((int64_t)b * Cin + ci) * H + ih) * W + iw];
-                    if (PRO) v = fmaxf(fmaf(v, pscale[ci], pshift[ci]), 0.f);
+            for (int j = 0; j < B_PER; ++j) {
+                const int r = lr_ld + j * RSTEP;
+                const int ci = ci_blk + r;
+                float v = 0.f;
+                if (inb && nb0 + r < Ntot) {
+                    v = src[(int64_t)ci * HWin];
+                    if (PRO) v = fmaxf(fmaf(v, s_sc[ci], s_sh[ci]), 0.f);
                 }
+                rb[j] = v;
             }
-            rb[j] = v;
+        } else {
+#pragma unroll
+            for (int j = 0; j < B_PER; ++j) {
+                const int n = nb0 + lr_ld + j * RSTEP;
+                float v = 0.f;
+                if (kv && n < Ntot) {
+                    const int tap = n / Cin, ci = n - tap * Cin;
+                    const int kh = tap / KS, kw = tap - kh * KS;
+                    const int ih = oh * ST - PADK + kh, iw = ow * ST - PADK + kw;
+                    if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+                        v = xb[(int64_t)ci * HWin + ih * W + iw];
+                        if (PRO) v = fmaxf(fmaf(v, s_sc[ci], s_sh[ci]), 0.f);
+                    }
+                }
+                rb[j] = v;
+            }
         }
     };
     auto store = [&](int buf) {
@@ -291,9 +396,9 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
         for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    float bsum = 0.f;  // bias-gradient row sum (threads < BM of n-tile-0 blocks)
+    float bsum = 0.f;
 
-    const int nkt = (int)((k_end - k_begin + BK - 1) / BK);
+    const int nkt = (int)((k_end - k_begin + WBK - 1) / WBK);
     if (nkt > 0) {
         load(k_begin);
         store(0);
@@ -302,13 +407,13 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
     const int li = lane & 31, lk = lane >> 5;
     for (int t = 0; t < nkt; ++t) {
         const int cur = t & 1;
-        if (t + 1 < nkt) load(k_begin + (int64_t)(t + 1) * BK);
+        if (t + 1 < nkt) load(k_begin + (int64_t)(t + 1) * WBK);
         if (bias_blk && tid < BM) {
 #pragma unroll 8
-            for (int kk = 0; kk < BK; ++kk) bsum += As[cur][kk][tid];
+            for (int kk = 0; kk < WBK; ++kk) bsum += As[cur][kk][tid];
         }
 #pragma unroll
-        for (int s = 0; s < BK / 2; ++s) {
+        for (int s = 0; s < WBK / 2; ++s) {
             float af[TM], bf[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i) af[i] = As[cur][2 * s + lk][wm + 32 * i + li];
@@ -342,9 +447,12 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
     if (bias_blk && tid < BM && m0 + tid < Cout) sl[(int64_t)(m0 + tid) * Nt + Ntot] = bsum;
 }
 
+// slab columns are tap-major (n = tap*Cin + ci); dw is the reference layout
+// [Cout][Cin][KS][KS] (ci*KS*KS + tap).
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Cout,
-                                                          int Ntot, int with_bias, float* __restrict__ dw,
+                                                          int Cin, int T, int with_bias, float* __restrict__ dw,
                                                           float* __restrict__ db, int accumulate) {
+    const int Ntot = Cin * T;
     const int Nt = Ntot + 1;
     const int64_t total = (int64_t)Cout * Nt;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -353,7 +461,8 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
         float s = 0.f;
         for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * total + i];
         if (n < Ntot) {
-            float* d = dw + (int64_t)m * Ntot + n;
+            const int tap = n / Cin, ci = n - tap * Cin;
+            float* d = dw + (int64_t)m * Ntot + (int64_t)ci * T + tap;
             *d = accumulate ? *d + s : s;
         } else if (db) {
             db[m] = accumulate ? db[m] + s : s;
@@ -361,46 +470,92 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     }
 }
 
-// wt[ci][co][kh][kw] = w[co][ci][KS-1-kh][KS-1-kw]
-__global__ void weight_flip_kernel(const float* __restrict__ w, int Cout, int Cin, int KS, float* __restrict__ wt) {
-    const int64_t total = (int64_t)Cout * Cin * KS * KS;
+// wt[co][tap][ci] = w[co][ci][tap]
+__global__ void tapmajor_kernel(const float* __restrict__ w, int Cout, int Cin, int T, float* __restrict__ wt) {
+    const int64_t total = (int64_t)Cout * Cin * T;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int kw = (int)(i % KS);
-        int64_t t = i / KS;
-        const int kh = (int)(t % KS);
-        t /= KS;
-        const int co = (int)(t % Cout);
-        const int ci = (int)(t / Cout);
-        wt[i] = w[(((int64_t)co * Cin + ci) * KS + (KS - 1 - kh)) * KS + (KS - 1 - kw)];
+        const int ci = (int)(i % Cin);
+        const int64_t t = i / Cin;
+        const int tap = (int)(t % T);
+        const int co = (int)(t / T);
+        wt[i] = w[((int64_t)co * Cin + ci) * T + tap];
     }
 }
 
-template <int BM, int BN, int KS, int ST, bool PRO, bool VECB>
+// dgrad weights, tap-major: wd[ci][tap][co] = w[co][ci][T-1-tap]
+__global__ void flip_tapmajor_kernel(const float* __restrict__ w, int Cout, int Cin, int T, float* __restrict__ wd) {
+    const int64_t total = (int64_t)Cout * Cin * T;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int co = (int)(i % Cout);
+        const int64_t t = i / Cout;
+        const int tap = (int)(t % T);
+        const int ci = (int)(t / T);
+        wd[i] = w[((int64_t)co * Cin + ci) * T + (T - 1 - tap)];
+    }
+}
+
+struct Plan {
+    int bm, splits, kchunk;
+};
+
+// Tile + split-K choice for the forward: aim for >= ~2 workgroups per CU.
+Plan fwd_plan(int Cout, int64_t N, int Ktot, int bn) {
+    Plan p;
+    p.bm = Cout >= 128 ? 128 : 64;
+    const int64_t tiles = ((Cout + p.bm - 1) / p.bm) * ((N + bn - 1) / bn);
+    const int nkt = (Ktot + BK - 1) / BK;
+    int s = 1;
+    if (tiles < 512) {
+        s = (int)((512 + tiles - 1) / tiles);
+        const int maxs = nkt / 2 > 0 ? nkt / 2 : 1;      // >= 2 K steps per split
+        if (s > maxs) s = maxs;
+    }
+    const int steps = (nkt + s - 1) / s;
+    p.kchunk = steps * BK;
+    p.splits = (nkt + steps - 1) / steps;
+    return p;
+}
+
+template <int BM, int BN, int KS, int ST, bool PRO, bool VECB, bool TAPK>
 int launch_fwd(const float* x, const float* w, const float* bias, const float* ps, const float* sh, const float* res,
-               float* y, int B, int Cin, int H, int W, int Cout, int Ho, int Wo, hipStream_t st) {
+               float* y, int B, int Cin, int H, int W, int Cout, int Ho, int Wo, const Plan& pl, float* slab,
+               hipStream_t st) {
     const int64_t N = (int64_t)B * Ho * Wo;
-    dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM));
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, 16, KS, ST, PRO, VECB>), grid, dim3(NT), 0, st, x, w, bias, ps, sh,
-                       res, y, B, Cin, H, W, Cout, Ho, Wo);
+    dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
+    const bool split = pl.splits > 1;
+    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, KS, ST, PRO, VECB, TAPK>), grid, dim3(NT), 0, st, x, w, bias, ps, sh,
+                       split ? nullptr : res, y, B, Cin, H, W, Cout, Ho, Wo, pl.kchunk, split ? slab : nullptr);
     UBPL_LAUNCH_CHECK();
+    if (split) {
+        const int64_t total = (int64_t)Cout * N;
+        int g = (int)((total + 255) / 256);
+        if (g > 8192) g = 8192;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, slab, pl.splits, Cout, Ho * Wo, N, bias,
+                           res, y);
+        UBPL_LAUNCH_CHECK();
+    }
     return 0;
 }
 
-template <int BM, int BN, int KS, int ST, bool PRO, bool VECB>
-int fwd_bm(bool big, const float* x, const float* w, const float* bias, const float* ps, const float* sh,
-           const float* res, float* y, int B, int Cin, int H, int W, int Cout, int Ho, int Wo, hipStream_t st) {
-    if (big) return launch_fwd<128, BN, KS, ST, PRO, VECB>(x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo, st);
-    return launch_fwd<64, BN, KS, ST, PRO, VECB>(x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo, st);
+template <int KS, int ST, bool PRO, bool VECB, bool TAPK>
+int fwd_bm(const Plan& pl, const float* x, const float* w, const float* bias, const float* ps, const float* sh,
+           const float* res, float* y, int B, int Cin, int H, int W, int Cout, int Ho, int Wo, float* slab,
+           hipStream_t st) {
+    if (pl.bm == 128)
+        return launch_fwd<128, 128, KS, ST, PRO, VECB, TAPK>(x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo,
+                                                            pl, slab, st);
+    return launch_fwd<64, 128, KS, ST, PRO, VECB, TAPK>(x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo, pl,
+                                                       slab, st);
 }
 
-template <int KS, int ST, bool PRO>
+template <int KS, int ST, bool PRO, bool TAPN>
 int wgrad_launch(const float* dy, const float* x, const float* ps, const float* sh, int B, int Cin, int H, int W,
                  int Cout, int Ho, int Wo, int splits, int kchunk, float* slab, int with_bias, hipStream_t st) {
     constexpr int BM = 64, BN = 64;
     const int Ntot = Cin * KS * KS;
     dim3 grid((unsigned)((Ntot + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM), (unsigned)splits);
-    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, 32, KS, ST, PRO>), grid, dim3(NT), 0, st, dy, x, ps, sh, B, Cin, H,
-                       W, Cout, Ho, Wo, kchunk, slab, with_bias);
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, KS, ST, PRO, TAPN>), grid, dim3(NT), 0, st, dy, x, ps, sh, B, Cin,
+                       H, W, Cout, Ho, Wo, kchunk, slab, with_bias);
     UBPL_LAUNCH_CHECK();
     return 0;
 }
@@ -408,8 +563,8 @@ int wgrad_launch(const float* dy, const float* x, const float* ps, const float* 
 void wgrad_plan(int B, int Cin, int Cout, int KS, int Ho, int Wo, int* splits, int* kchunk) {
     const int64_t K = (int64_t)B * Ho * Wo;
     const int64_t tiles = (int64_t)((Cin * KS * KS + 63) / 64) * ((Cout + 63) / 64);
-    int64_t want = (1024 + tiles - 1) / tiles;            // ~1024 workgroups
-    int64_t maxs = (K + 255) / 256;                       // >= 256 k per split
+    int64_t want = (1024 + tiles - 1) / tiles;
+    int64_t maxs = (K + 255) / 256;
     if (want > maxs) want = maxs;
     if (want < 1) want = 1;
     int64_t chunk = (K + want - 1) / want;
@@ -420,30 +575,43 @@ void wgrad_plan(int B, int Cin, int Cout, int KS, int Ho, int Wo, int* splits, i
 
 }  // namespace
 
-// y[B,Cout,Ho,Wo] = conv(relu(x*pscale + pshift) or x, w[Cout,Cin,KS,KS], pad=(KS-1)/2) + bias (+ res).
-// Supported (KS, stride): (1,1), (3,1), (7,2).  res may alias y (in-place add).
+// Floats of workspace ubpl_conv2d_forward needs (split-K slab); 0 = none.
+// w must be in the layout of ubpl_conv_weight_tapmajor for KS > 1.
+UBPL_API int64_t ubpl_conv2d_forward_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo) {
+    const int64_t N = (int64_t)B * Ho * Wo;
+    const Plan pl = fwd_plan(Cout, N, Cin * KS * KS, 128);
+    return pl.splits > 1 ? (int64_t)pl.splits * Cout * N : 0;
+}
+
+// y[B,Cout,Ho,Wo] = conv(relu(x*pscale + pshift) or x, w~, pad=(KS-1)/2) + bias (+ res).
+// w~: [Cout][Cin] for KS == 1, tap-major [Cout][KS*KS][Cin] otherwise.
+// Supported (KS, stride): (1,1), (3,1), (7,2).  res may alias y.  slab: the
+// workspace of ubpl_conv2d_forward_workspace (nullable when that is 0).
 UBPL_API int ubpl_conv2d_forward(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias,
                                  int Cout, int KS, int stride, const float* pscale, const float* pshift,
-                                 const float* res, float* y, int Ho, int Wo, void* stream) {
+                                 const float* res, float* y, int Ho, int Wo, float* slab, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const bool pro = pscale != nullptr;
-    const bool big = Cout >= 128;
+    if (pro && Cin > MAXC) return (int)hipErrorInvalidValue;
+    const int64_t N = (int64_t)B * Ho * Wo;
+    const Plan pl = fwd_plan(Cout, N, Cin * KS * KS, 128);
+    if (pl.splits > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
     if (KS == 1 && stride == 1) {
         const bool vec = ((Ho * Wo) % 4 == 0) && (((uintptr_t)x & 15) == 0);
-        if (vec) {
-            if (pro) return fwd_bm<128, 128, 1, 1, true, true>(big, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, st);
-            return fwd_bm<128, 128, 1, 1, false, true>(big, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, st);
-        }
-        if (pro) return fwd_bm<128, 128, 1, 1, true, false>(big, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, st);
-        return fwd_bm<128, 128, 1, 1, false, false>(big, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, st);
+        if (vec)
+            return pro ? fwd_bm<1, 1, true, true, true>(pl, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st)
+                       : fwd_bm<1, 1, false, true, true>(pl, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st);
+        return pro ? fwd_bm<1, 1, true, false, true>(pl, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st)
+                   : fwd_bm<1, 1, false, false, true>(pl, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st);
     }
     if (KS == 3 && stride == 1) {
-        if (pro) return fwd_bm<128, 128, 3, 1, true, false>(big, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, st);
-        return fwd_bm<128, 128, 3, 1, false, false>(big, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, st);
+        if (Cin % BK != 0) return (int)hipErrorInvalidValue;
+        return pro ? fwd_bm<3, 1, true, false, true>(pl, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st)
+                   : fwd_bm<3, 1, false, false, true>(pl, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st);
     }
     if (KS == 7 && stride == 2) {
-        if (pro) return fwd_bm<64, 128, 7, 2, true, false>(false, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, st);
-        return fwd_bm<64, 128, 7, 2, false, false>(false, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, st);
+        return pro ? fwd_bm<7, 2, true, false, false>(pl, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st)
+                   : fwd_bm<7, 2, false, false, false>(pl, x, w, bias, pscale, pshift, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st);
     }
     return (int)hipErrorInvalidValue;
 }
@@ -461,39 +629,55 @@ UBPL_API int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, 
                                int stride, const float* pscale, const float* pshift, int Ho, int Wo, float* slab,
                                float* dw, float* db, int accumulate, void* stream) {
     hipStream_t st = (hipStream_t)stream;
+    if (pscale != nullptr && Cin > MAXC) return (int)hipErrorInvalidValue;
     int splits, kchunk;
     wgrad_plan(B, Cin, Cout, KS, Ho, Wo, &splits, &kchunk);
     const bool pro = pscale != nullptr;
     const int wb = db != nullptr;
+    const bool tapn = (KS == 1) || (Cin % 64 == 0);
     int rc;
     if (KS == 1 && stride == 1)
-        rc = pro ? wgrad_launch<1, 1, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
-                 : wgrad_launch<1, 1, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+        rc = pro ? wgrad_launch<1, 1, true, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
+                 : wgrad_launch<1, 1, false, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+    else if (KS == 3 && stride == 1 && tapn)
+        rc = pro ? wgrad_launch<3, 1, true, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
+                 : wgrad_launch<3, 1, false, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
     else if (KS == 3 && stride == 1)
-        rc = pro ? wgrad_launch<3, 1, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
-                 : wgrad_launch<3, 1, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+        rc = pro ? wgrad_launch<3, 1, true, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
+                 : wgrad_launch<3, 1, false, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
     else if (KS == 7 && stride == 2)
-        rc = pro ? wgrad_launch<7, 2, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
-                 : wgrad_launch<7, 2, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+        rc = pro ? wgrad_launch<7, 2, true, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
+                 : wgrad_launch<7, 2, false, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
     else
         return (int)hipErrorInvalidValue;
     if (rc) return rc;
-    const int Ntot = Cin * KS * KS;
-    const int64_t total = (int64_t)Cout * (Ntot + 1);
+    const int64_t total = (int64_t)Cout * (Cin * KS * KS + 1);
     int grid = (int)((total + 255) / 256);
     if (grid > 4096) grid = 4096;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, st, slab, splits, Cout, Ntot, wb, dw, db,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, st, slab, splits, Cout, Cin, KS * KS, wb, dw, db,
                        accumulate);
     UBPL_LAUNCH_CHECK();
     return 0;
 }
 
-// wt = transpose(flip(w)) so that dgrad(stride 1) = conv(dy, wt).
+// Forward weight layout for KS > 1: wt[co][tap][ci] = w[co][ci][tap].
+UBPL_API int ubpl_conv_weight_tapmajor(const float* w, int Cout, int Cin, int KS, float* wt, void* stream) {
+    const int64_t total = (int64_t)Cout * Cin * KS * KS;
+    int grid = (int)((total + 255) / 256);
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(tapmajor_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, KS * KS, wt);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// dgrad weights (stride 1): wd[ci][tap][co] = w[co][ci][KS*KS-1-tap], i.e. the
+// tap-major forward layout of the flipped, transposed kernel: dx = conv(dy, wd).
 UBPL_API int ubpl_conv_weight_flip(const float* w, int Cout, int Cin, int KS, float* wt, void* stream) {
     const int64_t total = (int64_t)Cout * Cin * KS * KS;
     int grid = (int)((total + 255) / 256);
     if (grid > 4096) grid = 4096;
-    hipLaunchKernelGGL(weight_flip_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, KS, wt);
+    hipLaunchKernelGGL(flip_tapmajor_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, KS * KS,
+                       wt);
     UBPL_LAUNCH_CHECK();
     return 0;
 }

@@ -231,15 +231,32 @@ def conv_out_hw(H, W, KS, stride):
     return (H + 2 * pad - KS) // stride + 1, (W + 2 * pad - KS) // stride + 1
 
 
-def conv2d_forward(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out=None):
+def conv_weight_tapmajor(w):
+    Cout, Cin, KS, _ = w.shape
+    wt = torch.empty((Cout, KS * KS, Cin), device=w.device, dtype=F32)
+    call("ubpl_conv_weight_tapmajor", _p(w), Cout, Cin, KS, _p(wt), stream())
+    return wt
+
+
+def conv2d_forward(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out=None, w_tap=None):
+    """w: reference layout [Cout,Cin,KS,KS] (re-laid out tap-major here for
+    KS > 1) — or pass w_tap, an already tap-major [Cout,KS*KS,Cin] copy."""
     B, Cin, H, W = x.shape
-    Cout, wc, KS, _ = w.shape
+    if w_tap is not None:
+        Cout, T, wc = w_tap.shape
+        KS = int(round(T ** 0.5))
+        wk = w_tap
+    else:
+        Cout, wc, KS, _ = w.shape
+        wk = w if KS == 1 else conv_weight_tapmajor(w)
     if wc != Cin:
         raise AssertionError("{} {}".format(Cin, wc))  # models/base/layers.py:44
     Ho, Wo = conv_out_hw(H, W, KS, stride)
     y = torch.empty((B, Cout, Ho, Wo), device=x.device, dtype=F32) if out is None else out
-    call("ubpl_conv2d_forward", _p(x), B, Cin, H, W, _p(w), _p(bias), Cout, KS, stride, _p(pscale), _p(pshift),
-         _p(res), _p(y), Ho, Wo, stream())
+    nws = _lib.lib().ubpl_conv2d_forward_workspace(B, Cin, Cout, KS, Ho, Wo)
+    slab = torch.empty(int(nws), device=x.device, dtype=F32) if nws > 0 else None
+    call("ubpl_conv2d_forward", _p(x), B, Cin, H, W, _p(wk), _p(bias), Cout, KS, stride, _p(pscale), _p(pshift),
+         _p(res), _p(y), Ho, Wo, _p(slab), stream())
     return y
 
 
@@ -253,8 +270,9 @@ def conv2d_wgrad(dy, x, KS, stride, dw, db, pscale=None, pshift=None, accumulate
 
 
 def conv_weight_flip(w):
+    """Tap-major [Cin, KS*KS, Cout] weights of the data gradient (stride 1)."""
     Cout, Cin, KS, _ = w.shape
-    wt = torch.empty((Cin, Cout, KS, KS), device=w.device, dtype=F32)
+    wt = torch.empty((Cin, KS * KS, Cout), device=w.device, dtype=F32)
     call("ubpl_conv_weight_flip", _p(w), Cout, Cin, KS, _p(wt), stream())
     return wt
 
@@ -263,7 +281,7 @@ def conv2d_dgrad(dy, w, res=None, out=None, wt=None):
     """dx of a stride-1 conv = conv(dy, flip(w)^T); res/out allow accumulation."""
     if wt is None:
         wt = conv_weight_flip(w)
-    return conv2d_forward(dy, wt, None, 1, res=res, out=out)
+    return conv2d_forward(dy, None, None, 1, res=res, out=out, w_tap=wt)
 
 
 # ------------------------------------------------------------------ pool / upsample
