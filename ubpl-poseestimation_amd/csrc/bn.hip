@@ -121,6 +121,7 @@ __global__ void __launch_bounds__(256) apply_kernel(const float* __restrict__ x,
     }
 }
 
+template <bool VEC>
 __global__ void __launch_bounds__(256) bwd_partial_kernel(const float* __restrict__ dz, const float* __restrict__ x,
                                                          int B, int C, int HW, int bper,
                                                          const float* __restrict__ scale,
@@ -134,12 +135,29 @@ __global__ void __launch_bounds__(256) bwd_partial_kernel(const float* __restric
     float s1 = 0.f, s2 = 0.f;
     for (int b = b0; b < b1; ++b) {
         const int64_t off = ((int64_t)b * C + c) * HW;
-        for (int i = threadIdx.x; i < HW; i += blockDim.x) {
-            const float xv = x[off + i];
-            float g = dz[off + i];
-            if (relu && !(fmaf(xv, sc, sh) > 0.f)) g = 0.f;
-            s1 += g;
-            s2 = fmaf(g, xv - mu, s2);
+        if (VEC) {
+            const float4* x4 = reinterpret_cast<const float4*>(x + off);
+            const float4* d4 = reinterpret_cast<const float4*>(dz + off);
+            for (int i = threadIdx.x; i < (HW >> 2); i += blockDim.x) {
+                const float4 xv = x4[i];
+                float4 g = d4[i];
+                if (relu) {
+                    g.x = fmaf(xv.x, sc, sh) > 0.f ? g.x : 0.f;
+                    g.y = fmaf(xv.y, sc, sh) > 0.f ? g.y : 0.f;
+                    g.z = fmaf(xv.z, sc, sh) > 0.f ? g.z : 0.f;
+                    g.w = fmaf(xv.w, sc, sh) > 0.f ? g.w : 0.f;
+                }
+                s1 += (g.x + g.y) + (g.z + g.w);
+                s2 = fmaf(g.x, xv.x - mu, fmaf(g.y, xv.y - mu, fmaf(g.z, xv.z - mu, fmaf(g.w, xv.w - mu, s2))));
+            }
+        } else {
+            for (int i = threadIdx.x; i < HW; i += blockDim.x) {
+                const float xv = x[off + i];
+                float g = dz[off + i];
+                if (relu && !(fmaf(xv, sc, sh) > 0.f)) g = 0.f;
+                s1 += g;
+                s2 = fmaf(g, xv - mu, s2);
+            }
         }
     }
     const double d1 = ubpl::block_sum((double)s1, red);
@@ -169,9 +187,46 @@ __global__ void bwd_finalize_kernel(const double* __restrict__ part, int C, int 
     cc[c] = (float)(-g * is * s1 / (double)N);
 }
 
-__global__ void __launch_bounds__(256) bwd_apply_kernel(const float* __restrict__ dz, const float* __restrict__ x,
-                                                       int C, int HW, int64_t total,
-                                                       const float* __restrict__ scale,
+__device__ __forceinline__ float bwd_one(float g, float xv, float sc, float sh, float mu, float a, float b, float c,
+                                         int relu) {
+    if (relu && !(fmaf(xv, sc, sh) > 0.f)) g = 0.f;
+    return fmaf(a, g, fmaf(b, xv - mu, c));
+}
+
+// HW % 4 == 0: float4 lanes, one channel per 4-vector.  total4 = B*C*HW/4.
+__global__ void __launch_bounds__(256) bwd_apply_vec_kernel(const float* dz, const float* __restrict__ x, int C,
+                                                           int HW4, int64_t total4, const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ mean, int relu,
+                                                           const float* __restrict__ ca,
+                                                           const float* __restrict__ cb,
+                                                           const float* __restrict__ cc, const float* add1,
+                                                           const float* add2, float* dx) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += stride) {
+        const int c = (int)((i / HW4) % C);
+        const float sc = scale[c], sh = shift[c], mu = mean[c], a = ca[c], b = cb[c], cx = cc[c];
+        const float4 xv = reinterpret_cast<const float4*>(x)[i];
+        const float4 g = reinterpret_cast<const float4*>(dz)[i];
+        float4 v;
+        v.x = bwd_one(g.x, xv.x, sc, sh, mu, a, b, cx, relu);
+        v.y = bwd_one(g.y, xv.y, sc, sh, mu, a, b, cx, relu);
+        v.z = bwd_one(g.z, xv.z, sc, sh, mu, a, b, cx, relu);
+        v.w = bwd_one(g.w, xv.w, sc, sh, mu, a, b, cx, relu);
+        if (add1) {
+            const float4 q = reinterpret_cast<const float4*>(add1)[i];
+            v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+        }
+        if (add2) {
+            const float4 q = reinterpret_cast<const float4*>(add2)[i];
+            v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+        }
+        reinterpret_cast<float4*>(dx)[i] = v;
+    }
+}
+
+__global__ void __launch_bounds__(256) bwd_apply_kernel(const float* dz, const float* __restrict__ x, int C, int HW,
+                                                       int64_t total, const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const float* __restrict__ mean, int relu,
                                                        const float* __restrict__ ca, const float* __restrict__ cb,
@@ -180,10 +235,7 @@ __global__ void __launch_bounds__(256) bwd_apply_kernel(const float* __restrict_
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
         const int c = (int)((i / HW) % C);
-        const float xv = x[i];
-        float g = dz[i];
-        if (relu && !(fmaf(xv, scale[c], shift[c]) > 0.f)) g = 0.f;
-        float v = fmaf(ca[c], g, fmaf(cb[c], xv - mean[c], cc[c]));
+        float v = bwd_one(dz[i], x[i], scale[c], shift[c], mean[c], ca[c], cb[c], cc[c], relu);
         if (add1) v += add1[i];
         if (add2) v += add2[i];
         dx[i] = v;
@@ -261,8 +313,14 @@ UBPL_API int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int
     const int splits = splits_for(B, C);
     const int bper = (B + splits - 1) / splits;
     const int gs = (B + bper - 1) / bper;
-    hipLaunchKernelGGL(bwd_partial_kernel, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW, bper,
-                       scale, shift, mean, relu, part);
+    const uintptr_t al = (uintptr_t)dz | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)add1 | (uintptr_t)add2;
+    const bool vec = (HW % 4 == 0) && ((al & 15) == 0);
+    if (vec)
+        hipLaunchKernelGGL(bwd_partial_kernel<true>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
+                           bper, scale, shift, mean, relu, part);
+    else
+        hipLaunchKernelGGL(bwd_partial_kernel<false>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
+                           bper, scale, shift, mean, relu, part);
     UBPL_LAUNCH_CHECK();
     float* ca = coef;
     float* cb = coef + C;
@@ -271,8 +329,12 @@ UBPL_API int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int
                        (int64_t)B * HW, gamma, invstd, dgamma, dbeta, ca, cb, cc);
     UBPL_LAUNCH_CHECK();
     const int64_t total = (int64_t)B * C * HW;
-    hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_ew(total)), dim3(256), 0, (hipStream_t)stream, dz, x, C, HW, total,
-                       scale, shift, mean, relu, ca, cb, cc, add1, add2, dx);
+    if (vec)
+        hipLaunchKernelGGL(bwd_apply_vec_kernel, dim3(grid_ew(total / 4)), dim3(256), 0, (hipStream_t)stream, dz, x, C,
+                           HW / 4, total / 4, scale, shift, mean, relu, ca, cb, cc, add1, add2, dx);
+    else
+        hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_ew(total)), dim3(256), 0, (hipStream_t)stream, dz, x, C, HW,
+                           total, scale, shift, mean, relu, ca, cb, cc, add1, add2, dx);
     UBPL_LAUNCH_CHECK();
     return 0;
 }

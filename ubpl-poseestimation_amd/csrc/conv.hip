@@ -94,23 +94,31 @@ __global__ void __launch_bounds__(NT) conv_fwd_kernel(const float* __restrict__ 
     float ra[A_PER];
     float rb[B_PER];
 
+    // Loads are unconditional at a clamped (always valid) address and masked
+    // afterwards: a load under a per-element branch makes hipcc wait vmcnt(0)
+    // per element (cdna_hip_programming.md §5 'Three .s-level traps' (c)).
+    const int am_c = min(m0 + am, Cout - 1);
+    const bool am_ok = m0 + am < Cout;
+    const float* wrow = w + (int64_t)am_c * Ktot;
     auto load_a = [&](int kt) {
-        const int m = m0 + am;
         const int k = kt + ak0;
-        if (m < Cout && avec && k + A_PER <= k_end) {
-            const float4* src = reinterpret_cast<const float4*>(w + (int64_t)m * Ktot + k);
+        if (avec && k + A_PER <= k_end) {
+            const float4* src = reinterpret_cast<const float4*>(wrow + k);
 #pragma unroll
             for (int j = 0; j < A_PER / 4; ++j) {
                 const float4 v = src[j];
-                ra[4 * j] = v.x;
-                ra[4 * j + 1] = v.y;
-                ra[4 * j + 2] = v.z;
-                ra[4 * j + 3] = v.w;
+                ra[4 * j] = am_ok ? v.x : 0.f;
+                ra[4 * j + 1] = am_ok ? v.y : 0.f;
+                ra[4 * j + 2] = am_ok ? v.z : 0.f;
+                ra[4 * j + 3] = am_ok ? v.w : 0.f;
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < A_PER; ++j)
-                ra[j] = (m < Cout && k + j < k_end) ? w[(int64_t)m * Ktot + k + j] : 0.f;
+            for (int j = 0; j < A_PER; ++j) {
+                const int kk = k + j;
+                const float v = wrow[min(kk, Ktot - 1)];
+                ra[j] = (am_ok && kk < k_end) ? v : 0.f;
+            }
         }
     };
     auto load_b = [&](int kt) {
@@ -120,21 +128,20 @@ __global__ void __launch_bounds__(NT) conv_fwd_kernel(const float* __restrict__ 
 #pragma unroll
             for (int j = 0; j < BK / VROWS; ++j) {
                 const int k = kt + bk0 + j * VROWS;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (cvalid && k < k_end) {
-                    v = *reinterpret_cast<const float4*>(xb + (int64_t)k * P + p);
-                    if (PRO) {
-                        const float sc = s_sc[k], sh = s_sh[k];
-                        v.x = fmaxf(fmaf(v.x, sc, sh), 0.f);
-                        v.y = fmaxf(fmaf(v.y, sc, sh), 0.f);
-                        v.z = fmaxf(fmaf(v.z, sc, sh), 0.f);
-                        v.w = fmaxf(fmaf(v.w, sc, sh), 0.f);
-                    }
+                const bool ok = cvalid && k < k_end;
+                const int kc = min(k, Cin - 1);
+                float4 v = *reinterpret_cast<const float4*>(xb + (int64_t)kc * P + p);
+                if (PRO) {
+                    const float sc = s_sc[kc], sh = s_sh[kc];
+                    v.x = fmaxf(fmaf(v.x, sc, sh), 0.f);
+                    v.y = fmaxf(fmaf(v.y, sc, sh), 0.f);
+                    v.z = fmaxf(fmaf(v.z, sc, sh), 0.f);
+                    v.w = fmaxf(fmaf(v.w, sc, sh), 0.f);
                 }
-                rb[4 * j] = v.x;
-                rb[4 * j + 1] = v.y;
-                rb[4 * j + 2] = v.z;
-                rb[4 * j + 3] = v.w;
+                rb[4 * j] = ok ? v.x : 0.f;
+                rb[4 * j + 1] = ok ? v.y : 0.f;
+                rb[4 * j + 2] = ok ? v.z : 0.f;
+                rb[4 * j + 3] = ok ? v.w : 0.f;
             }
         } else if constexpr (TAPK) {
             // one tap for the whole K tile: input coordinates once per tile
@@ -142,16 +149,15 @@ __global__ void __launch_bounds__(NT) conv_fwd_kernel(const float* __restrict__ 
             const int kh = tap / KS, kw = tap - kh * KS;
             const int ih = coh * ST - PADK + kh, iw = cow * ST - PADK + kw;
             const bool inb = cvalid && ih >= 0 && ih < H && iw >= 0 && iw < W;
-            const float* src = xb + (int64_t)ci0 * HWin + (inb ? ih * W + iw : 0);
+            const float* src = xb + (inb ? ih * W + iw : 0);
 #pragma unroll
             for (int j = 0; j < B_PER; ++j) {
                 const int r = bk0 + j * (NT / BN);
-                float v = 0.f;
-                if (inb && kt + r < k_end) {
-                    v = src[(int64_t)r * HWin];
-                    if (PRO) v = fmaxf(fmaf(v, s_sc[ci0 + r], s_sh[ci0 + r]), 0.f);
-                }
-                rb[j] = v;
+                const bool ok = inb && kt + r < k_end;
+                const int ci = min(ci0 + r, Cin - 1);
+                float v = src[(int64_t)ci * HWin];
+                if (PRO) v = fmaxf(fmaf(v, s_sc[ci], s_sh[ci]), 0.f);
+                rb[j] = ok ? v : 0.f;
             }
         } else {
             // generic (stem, Cin = 3): tap and channel per element
@@ -336,17 +342,16 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
     auto load = [&](int64_t kt) {
         const int64_t k = kt + lk_ld;
         const bool kv = k < k_end;
-        int b = 0, p = 0, oh = 0, ow = 0;
-        if (kv) {
-            b = (int)(k / P);
-            p = (int)(k - (int64_t)b * P);
-            oh = p / Wo;
-            ow = p - oh * Wo;
-        }
+        const int64_t kc = kv ? k : k_begin;        // clamped, always valid
+        const int b = (int)(kc / P);
+        const int p = (int)(kc - (int64_t)b * P);
+        const int oh = p / Wo, ow = p - oh * Wo;
+        const float* dyb = dy + (int64_t)b * Cout * P + p;
 #pragma unroll
         for (int j = 0; j < A_PER; ++j) {
             const int m = m0 + lr_ld + j * RSTEP;
-            ra[j] = (kv && m < Cout) ? dy[((int64_t)b * Cout + m) * P + p] : 0.f;
+            const float v = dyb[(int64_t)min(m, Cout - 1) * P];
+            ra[j] = (kv && m < Cout) ? v : 0.f;
         }
         const float* xb = x + (int64_t)b * Cin * HWin;
         if constexpr (TAPN) {
@@ -356,13 +361,11 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
 #pragma unroll
             for (int j = 0; j < B_PER; ++j) {
                 const int r = lr_ld + j * RSTEP;
-                const int ci = ci_blk + r;
-                float v = 0.f;
-                if (inb && nb0 + r < Ntot) {
-                    v = src[(int64_t)ci * HWin];
-                    if (PRO) v = fmaxf(fmaf(v, s_sc[ci], s_sh[ci]), 0.f);
-                }
-                rb[j] = v;
+                const bool ok = inb && nb0 + r < Ntot;
+                const int ci = min(ci_blk + r, Cin - 1);
+                float v = src[(int64_t)ci * HWin];
+                if (PRO) v = fmaxf(fmaf(v, s_sc[ci], s_sh[ci]), 0.f);
+                rb[j] = ok ? v : 0.f;
             }
         } else {
 #pragma unroll
@@ -551,7 +554,7 @@ int fwd_bm(const Plan& pl, const float* x, const float* w, const float* bias, co
 template <int KS, int ST, bool PRO, bool TAPN>
 int wgrad_launch(const float* dy, const float* x, const float* ps, const float* sh, int B, int Cin, int H, int W,
                  int Cout, int Ho, int Wo, int splits, int kchunk, float* slab, int with_bias, hipStream_t st) {
-    constexpr int BM = 64, BN = 64;
+    constexpr int BM = 128, BN = 128;
     const int Ntot = Cin * KS * KS;
     dim3 grid((unsigned)((Ntot + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM), (unsigned)splits);
     hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, KS, ST, PRO, TAPN>), grid, dim3(NT), 0, st, dy, x, ps, sh, B, Cin,
@@ -561,10 +564,12 @@ int wgrad_launch(const float* dy, const float* x, const float* ps, const float* 
 }
 
 void wgrad_plan(int B, int Cin, int Cout, int KS, int Ho, int Wo, int* splits, int* kchunk) {
+    // 128x128 tiles; split K so the grid holds ~2-3 workgroups per CU while every
+    // split keeps >= 512 k (the slab written + re-read stays small next to the operands).
     const int64_t K = (int64_t)B * Ho * Wo;
-    const int64_t tiles = (int64_t)((Cin * KS * KS + 63) / 64) * ((Cout + 63) / 64);
-    int64_t want = (1024 + tiles - 1) / tiles;
-    int64_t maxs = (K + 255) / 256;
+    const int64_t tiles = (int64_t)((Cin * KS * KS + 127) / 128) * ((Cout + 127) / 128);
+    int64_t want = (640 + tiles - 1) / tiles;
+    int64_t maxs = K / 512;
     if (want > maxs) want = maxs;
     if (want < 1) want = 1;
     int64_t chunk = (K + want - 1) / want;
@@ -634,7 +639,7 @@ UBPL_API int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, 
     wgrad_plan(B, Cin, Cout, KS, Ho, Wo, &splits, &kchunk);
     const bool pro = pscale != nullptr;
     const int wb = db != nullptr;
-    const bool tapn = (KS == 1) || (Cin % 64 == 0);
+    const bool tapn = (KS == 1) || (Cin % 128 == 0);
     int rc;
     if (KS == 1 && stride == 1)
         rc = pro ? wgrad_launch<1, 1, true, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
