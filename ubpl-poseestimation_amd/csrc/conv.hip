@@ -554,7 +554,7 @@ int fwd_bm(const Plan& pl, const float* x, const float* w, const float* bias, co
 template <int KS, int ST, bool PRO, bool TAPN>
 int wgrad_launch(const float* dy, const float* x, const float* ps, const float* sh, int B, int Cin, int H, int W,
                  int Cout, int Ho, int Wo, int splits, int kchunk, float* slab, int with_bias, hipStream_t st) {
-    constexpr int BM = 128, BN = 128;
+    constexpr int BM = 64, BN = 64;
     const int Ntot = Cin * KS * KS;
     dim3 grid((unsigned)((Ntot + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM), (unsigned)splits);
     hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, KS, ST, PRO, TAPN>), grid, dim3(NT), 0, st, dy, x, ps, sh, B, Cin,
@@ -564,12 +564,12 @@ int wgrad_launch(const float* dy, const float* x, const float* ps, const float* 
 }
 
 void wgrad_plan(int B, int Cin, int Cout, int KS, int Ho, int Wo, int* splits, int* kchunk) {
-    // 128x128 tiles; split K so the grid holds ~2-3 workgroups per CU while every
-    // split keeps >= 512 k (the slab written + re-read stays small next to the operands).
+    // 64x64 tiles (measured faster than 128x128 here: 2x the occupancy); split K
+    // so the grid holds ~4 workgroups per CU, every split >= 256 k.
     const int64_t K = (int64_t)B * Ho * Wo;
-    const int64_t tiles = (int64_t)((Cin * KS * KS + 127) / 128) * ((Cout + 127) / 128);
-    int64_t want = (640 + tiles - 1) / tiles;
-    int64_t maxs = K / 512;
+    const int64_t tiles = (int64_t)((Cin * KS * KS + 63) / 64) * ((Cout + 63) / 64);
+    int64_t want = (1024 + tiles - 1) / tiles;
+    int64_t maxs = (K + 255) / 256;
     if (want > maxs) want = maxs;
     if (want < 1) want = 1;
     int64_t chunk = (K + want - 1) / want;
@@ -639,7 +639,7 @@ UBPL_API int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, 
     wgrad_plan(B, Cin, Cout, KS, Ho, Wo, &splits, &kchunk);
     const bool pro = pscale != nullptr;
     const int wb = db != nullptr;
-    const bool tapn = (KS == 1) || (Cin % 128 == 0);
+    const bool tapn = (KS == 1) || (Cin % 64 == 0);
     int rc;
     if (KS == 1 && stride == 1)
         rc = pro ? wgrad_launch<1, 1, true, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
