@@ -118,6 +118,9 @@ int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, int H, in
 /* Data-gradient weights (stride 1): the tap-major layout of the flipped,
  * transposed kernel, so dx = ubpl_conv2d_forward(dy, wt). */
 int ubpl_conv_weight_flip(const float* w, int Cout, int Cin, int KS, float* wt, void* stream);
+/* Both re-layouts for many convs in one launch: table int64 [nseg][5] =
+ * (src_off, dst_off, Cout, Cin, KS*KS) in floats; mode 0 tap-major, 1 dgrad. */
+int ubpl_conv_weights_relayout(const float* src, float* dst, const int64_t* table, int nseg, int mode, void* stream);
 
 /* MaxPool2d(2,2) (models/base/layers.py:93), Upsample(x2, nearest) + add
  * (layers.py:110-111), AvgPool2d(2,2) projection (models/pose/hourglass.py:226). */

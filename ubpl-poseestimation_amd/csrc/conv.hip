@@ -497,6 +497,33 @@ __global__ void flip_tapmajor_kernel(const float* __restrict__ w, int Cout, int 
     }
 }
 
+// Batched weight re-layout over a segment table (int64 [nseg][5]:
+// src_off, dst_off, Cout, Cin, T), one segment per blockIdx.y.
+// mode 0: tap-major forward layout  dst[co][tap][ci] = src[co][ci][tap]
+// mode 1: dgrad layout               dst[ci][tap][co] = src[co][ci][T-1-tap]
+__global__ void __launch_bounds__(256) relayout_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                      const int64_t* __restrict__ table, int mode) {
+    const int64_t* e = table + (int64_t)blockIdx.y * 5;
+    const int64_t so = e[0], dof = e[1];
+    const int Cout = (int)e[2], Cin = (int)e[3], T = (int)e[4];
+    const int64_t total = (int64_t)Cout * Cin * T;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        if (mode == 0) {
+            const int ci = (int)(i % Cin);
+            const int64_t t = i / Cin;
+            const int tap = (int)(t % T);
+            const int co = (int)(t / T);
+            dst[dof + i] = src[so + ((int64_t)co * Cin + ci) * T + tap];
+        } else {
+            const int co = (int)(i % Cout);
+            const int64_t t = i / Cout;
+            const int tap = (int)(t % T);
+            const int ci = (int)(t / T);
+            dst[dof + i] = src[so + ((int64_t)co * Cin + ci) * T + (T - 1 - tap)];
+        }
+    }
+}
+
 struct Plan {
     int bm, splits, kchunk;
 };
@@ -570,6 +597,10 @@ void wgrad_plan(int B, int Cin, int Cout, int KS, int Ho, int Wo, int* splits, i
     const int64_t tiles = (int64_t)((Cin * KS * KS + 63) / 64) * ((Cout + 63) / 64);
     int64_t want = (1024 + tiles - 1) / tiles;
     int64_t maxs = (K + 255) / 256;
+    // keep the slab (splits * Cout * (Ntot+1) floats, written + re-read) no larger
+    // than the operands it is computed from (dy and x: K * (Cout + Cin) floats)
+    const int64_t cap = (K * (Cout + Cin)) / ((int64_t)Cout * (Cin * KS * KS + 1));
+    if (maxs > cap) maxs = cap;
     if (want > maxs) want = maxs;
     if (want < 1) want = 1;
     int64_t chunk = (K + want - 1) / want;
@@ -683,6 +714,15 @@ UBPL_API int ubpl_conv_weight_flip(const float* w, int Cout, int Cin, int KS, fl
     if (grid > 4096) grid = 4096;
     hipLaunchKernelGGL(flip_tapmajor_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, KS * KS,
                        wt);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// All conv weights of a model re-laid out in one launch (see relayout_kernel).
+UBPL_API int ubpl_conv_weights_relayout(const float* src, float* dst, const int64_t* table, int nseg, int mode,
+                                        void* stream) {
+    if (nseg <= 0) return 0;
+    hipLaunchKernelGGL(relayout_kernel, dim3(64, nseg), dim3(256), 0, (hipStream_t)stream, src, dst, table, mode);
     UBPL_LAUNCH_CHECK();
     return 0;
 }

@@ -38,6 +38,7 @@ SIGNATURES = {
     "ubpl_conv2d_wgrad_workspace": (L, [I, I, I, I, I, I]),
     "ubpl_conv2d_wgrad": (I, [P, P, I, I, I, I, I, I, I, P, P, I, I, P, P, P, I, P]),
     "ubpl_conv_weight_flip": (I, [P, I, I, I, P, P]),
+    "ubpl_conv_weights_relayout": (I, [P, P, P, I, I, P]),
     "ubpl_maxpool2x2_forward": (I, [P, L, I, I, P, P]),
     "ubpl_maxpool2x2_backward": (I, [P, P, L, I, I, P, I, P]),
     "ubpl_avgpool2x2_forward": (I, [P, L, I, I, P, P]),

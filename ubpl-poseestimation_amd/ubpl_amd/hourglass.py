@@ -179,6 +179,21 @@ class StackedHourglass(nn.Module):
                 mod.register_buffer("num_batches_tracked", self._nbt[self._bn_index[b]])
         self._grad_views_attached = False
         self._ws = {}
+        # re-laid-out conv weights, rebuilt by one launch per forward (tap-major
+        # [Cout][T][Cin] for KS > 1) and per backward (dgrad [Cin][T][Cout])
+        self._wlay = {}
+        for mode, keep in ((0, lambda ks, nm: ks > 1), (1, lambda ks, nm: nm != "pre.0.conv.weight")):
+            rows, idx, o = [], {}, 0
+            for name, shape, kind, live in tab:
+                if kind != "cw" or not live or not keep(shape[2], name):
+                    continue
+                s, n, _ = offs[name]
+                rows.append((s, o, shape[0], shape[1], shape[2] * shape[3]))
+                T = shape[2] * shape[3]
+                idx[name] = (o, (shape[0], T, shape[1]) if mode == 0 else (shape[1], T, shape[0]))
+                o += (n + 3) // 4 * 4
+            tbl = torch.tensor(rows, dtype=torch.int64).to(device)
+            self._wlay[mode] = (tbl, torch.empty(max(o, 4), device=device), idx)
 
     # -- structure helpers ------------------------------------------------
     def _node_for(self, name):
@@ -209,6 +224,15 @@ class StackedHourglass(nn.Module):
     def stats(self, bn):
         s, c = self._sidx[bn]
         return self.flat_stats[s:s + c], self.flat_stats[s + c:s + 2 * c]
+
+    def relayout_weights(self, mode):
+        tbl, buf, _ = self._wlay[mode]
+        Kn.conv_weights_relayout(self.flat_params, buf, tbl, mode)
+
+    def W(self, mode, name):
+        _, buf, idx = self._wlay[mode]
+        o, shp = idx[name]
+        return buf[o:o + shp[0] * shp[1] * shp[2]].view(shp)
 
     def live_params(self):
         return self.flat_params[:self.n_live]
@@ -267,6 +291,7 @@ class StackedHourglass(nn.Module):
         dev = imgs.device
         part = self._scratch(B, 64)
         ex = _Exec(self, B, dev, part, train=self.training, save=save)
+        self.relayout_weights(0)
         if self.training:
             self._nbt.add_(1)
         else:
@@ -372,7 +397,8 @@ class _Exec:
         w = self.m.P(name + ".weight")
         b = self.m.P(name + ".bias")
         ps, ph = (None, None) if pro is None else pro
-        return Kn.conv2d_forward(x, w, b, stride, ps, ph, res=res, out=out)
+        wt = self.m.W(0, name + ".weight") if w.shape[2] > 1 else None
+        return Kn.conv2d_forward(x, w, b, stride, ps, ph, res=res, out=out, w_tap=wt)
 
     # ---- layers
     def stem(self, imgs):
@@ -431,7 +457,7 @@ class _Exec:
                         accumulate=True)
 
     def dgrad(self, name, dy, res=None, out=None):
-        return Kn.conv2d_dgrad(dy, self.m.P(name + ".weight"), res=res, out=out)
+        return Kn.conv2d_dgrad(dy, None, res=res, out=out, wt=self.m.W(1, name + ".weight"))
 
     def residual_bwd(self, p, dout):
         x, t1, t2 = self.saved.get(p)
@@ -469,6 +495,7 @@ class _Exec:
     def backward(self, dpreds, dfeats):
         m = self.m
         S = m.nStack
+        m.relayout_weights(1)
         dpreds = dpreds.contiguous()
         if dfeats is not None:
             dfeats = dfeats.contiguous()

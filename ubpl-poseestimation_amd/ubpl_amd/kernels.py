@@ -277,6 +277,11 @@ def conv_weight_flip(w):
     return wt
 
 
+def conv_weights_relayout(src, dst, table, mode):
+    """table: int64 [nseg,5] device tensor (src_off, dst_off, Cout, Cin, T)."""
+    call("ubpl_conv_weights_relayout", _p(src), _p(dst), _p(table), int(table.shape[0]), int(mode), stream())
+
+
 def conv2d_dgrad(dy, w, res=None, out=None, wt=None):
     """dx of a stride-1 conv = conv(dy, flip(w)^T); res/out allow accumulation."""
     if wt is None:

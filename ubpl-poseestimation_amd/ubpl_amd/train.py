@@ -136,6 +136,16 @@ def _sync_stats(local_sums, counts):
 # ---------------------------------------------------------------------------
 # MT_UBPL
 # ---------------------------------------------------------------------------
+def _backward_all(totals):
+    """The reference runs total_i.backward(retain_graph=True) once per student
+    (projects/MT_UBPL.py:334-336): the shared FDL term makes every call reach
+    every student, so each network's backward would run M times with gradients
+    that are then summed into .grad.  Backward is linear, so one traversal of
+    sum_i total_i accumulates the same gradients with each network's backward
+    run once (its upstream gradients summed first)."""
+    torch.autograd.backward(totals)
+
+
 def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
     """projects/MT_UBPL.py:157-352 -> (pec_records, mtc_records, epc_records, fdc_record)."""
     M = len(models)
@@ -214,8 +224,7 @@ def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
             epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[3 * mi + 1])
             totals.append(pec + mtc + epc + fdc)
             rec.append((pec, mtc, epc))
-        for t in totals:                                          # :334-336
-            t.backward(retain_graph=True)
+        _backward_all(totals)                                     # :334-336
         D.allreduce_grads(models)
         for o in optims:
             o.step()
@@ -322,8 +331,7 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
             pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[6 * mi + 1])
             epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2])
             totals.append(pec + mtc + epc + fdc)
-        for t in totals:
-            t.backward(retain_graph=True)
+        _backward_all(totals)                                     # DualPose_UBPL.py:277-279
         D.allreduce_grads(models)
         for o in optims:
             o.step()
