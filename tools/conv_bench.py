@@ -4,8 +4,8 @@ For every distinct conv shape of StackedHourglass(16, 2) at batch B, times the
 forward (with its BN prologue when the network has one), the data gradient and
 the weight gradient through the C-ABI, and prints ms/call, TFLOP/s and the
 per-step contribution (calls per step x ms).  A student step = fwd + dgrad +
-wgrad; the teacher forward adds one fwd per conv (MT_UBPL: 2 students,
-2 teachers per step in bench.py's workload).
+wgrad; the teacher forward adds one fwd per conv (MT_UBPL, 2 views: 8
+forwards and 4 backwards per step in bench.py's workload).
 
     python tools/conv_bench.py [B] [reps]
 """
@@ -89,8 +89,8 @@ def main():
             wd = Kn.conv_weight_flip(w)
             dx = torch.empty_like(x)
             td = timeit(lambda: Kn.conv2d_dgrad(y, None, out=dx, wt=wd), reps)
-        # per MT_UBPL step: 4 forwards (2 students + 2 teachers), 2 backwards
-        step = {"fwd": 4 * cnt * tf, "dgrad": 2 * cnt * (0 if td != td else td), "wgrad": 2 * cnt * tw}
+        # per MT_UBPL step (2 views): 8 forwards (2 students + 2 teachers), 4 backwards
+        step = {"fwd": 8 * cnt * tf, "dgrad": 4 * cnt * (0 if td != td else td), "wgrad": 4 * cnt * tw}
         for kx in tot:
             tot[kx] += step[kx]
         rows.append((cin, cout, ks, st, h, pro, cnt, tf, fl / tf / 1e9, td, fl / td / 1e9 if td == td else 0.0, tw,

@@ -40,7 +40,7 @@ constexpr int MAXC = 256;  // largest Cin with a fused BN prologue
 // ------------------------------------------------------------------ forward
 // TAPK: k tiles never straddle a tap (Cin % BK == 0 or KS == 1).
 template <int BM, int BN, int KS, int ST, bool PRO, bool VECB, bool TAPK>
-__global__ void __launch_bounds__(NT) conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+__global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ bias,
                                                      const float* __restrict__ pscale,
                                                      const float* __restrict__ pshift, const float* res, float* y,
@@ -528,22 +528,69 @@ struct Plan {
     int bm, splits, kchunk;
 };
 
-// Tile + split-K choice for the forward: aim for >= ~2 workgroups per CU.
-Plan fwd_plan(int Cout, int64_t N, int Ktot, int bn) {
-    Plan p;
-    p.bm = Cout >= 128 ? 128 : 64;
-    const int64_t tiles = ((Cout + p.bm - 1) / p.bm) * ((N + bn - 1) / bn);
-    const int nkt = (Ktot + BK - 1) / BK;
-    int s = 1;
-    if (tiles < 512) {
-        s = (int)((512 + tiles - 1) / tiles);
-        const int maxs = nkt / 2 > 0 ? nkt / 2 : 1;      // >= 2 K steps per split
-        if (s > maxs) s = maxs;
+// ---- grid planning: a cost model over whole CU rounds.
+// Blocks spread evenly over the CUs; a CU with c blocks (r = min(c, occ)
+// resident) runs them in c * (steps + 2) K steps at a rate that needs ~3
+// resident blocks to hide latency.  Split-K adds the slab written by the
+// main kernel and re-read by the reduce, plus one launch.
+struct Device {
+    int ncu = 256;
+    int occ_fwd128 = 4, occ_fwd64 = 5, occ_wgrad = 4;
+};
+
+const Device& device_info();
+
+double split_cost(int64_t tiles, int s, int64_t nsteps, int occ, int ncu, double step_flops, double slab_bytes_per_split) {
+    const int64_t blocks = tiles * s;
+    const int64_t per_cu = (blocks + ncu - 1) / ncu;
+    const int64_t r = per_cu < occ ? per_cu : occ;
+    const double eff = r >= 3 ? 1.0 : (r + 1) / 4.0;
+    const int64_t steps = (nsteps + s - 1) / s;
+    const double rate = 0.6e12 * 0.8;             // f32 MFMA flop/s per CU, sustained
+    double t = (double)per_cu * (double)(steps + 2) * step_flops / (rate * eff);
+    if (s > 1) t += 2.0 * s * slab_bytes_per_split / 5e12 + 4e-6;
+    return t;
+}
+
+int best_split(int64_t tiles, int64_t nsteps, int maxs, int occ, int ncu, double step_flops,
+               double slab_bytes_per_split) {
+    int best = 1;
+    double bc = split_cost(tiles, 1, nsteps, occ, ncu, step_flops, slab_bytes_per_split);
+    for (int s = 2; s <= maxs; ++s) {
+        const double c = split_cost(tiles, s, nsteps, occ, ncu, step_flops, slab_bytes_per_split);
+        if (c < bc * 0.97) {      // a split must pay for itself clearly
+            bc = c;
+            best = s;
+        }
     }
-    const int steps = (nkt + s - 1) / s;
-    p.kchunk = steps * BK;
-    p.splits = (nkt + steps - 1) / steps;
-    return p;
+    return best;
+}
+
+// Tile height + split-K for the forward (BN = 128, BK = 16).
+Plan fwd_plan(int Cout, int64_t N, int Ktot, int bn) {
+    const Device& d = device_info();
+    const int nkt = (Ktot + BK - 1) / BK;
+    const int maxs = nkt / 2 > 0 ? nkt / 2 : 1;            // >= 2 K steps per split
+    Plan best{64, 1, 0};
+    double bc = 1e30;
+    for (int bm : {128, 64}) {
+        if (bm == 128 && Cout <= 64) continue;
+        const int64_t tiles = ((Cout + bm - 1) / bm) * ((N + bn - 1) / bn);
+        const int occ = bm == 128 ? d.occ_fwd128 : d.occ_fwd64;
+        const double sf = 2.0 * bm * bn * BK;
+        const int s = best_split(tiles, nkt, maxs, occ, d.ncu, sf, 4.0 * Cout * N);
+        // 64-row tiles re-read the B operand twice as often: ~15% slower per flop (measured)
+        const double c = split_cost(tiles, s, nkt, occ, d.ncu, sf, 4.0 * Cout * N) / (bm == 128 ? 1.0 : 0.85);
+        if (c < bc) {
+            bc = c;
+            best.bm = bm;
+            best.splits = s;
+        }
+    }
+    const int steps = (nkt + best.splits - 1) / best.splits;
+    best.kchunk = steps * BK;
+    best.splits = (nkt + steps - 1) / steps;
+    return best;
 }
 
 template <int BM, int BN, int KS, int ST, bool PRO, bool VECB, bool TAPK>
@@ -591,22 +638,49 @@ int wgrad_launch(const float* dy, const float* x, const float* ps, const float* 
 }
 
 void wgrad_plan(int B, int Cin, int Cout, int KS, int Ho, int Wo, int* splits, int* kchunk) {
-    // 64x64 tiles (measured faster than 128x128 here: 2x the occupancy); split K
-    // so the grid holds ~4 workgroups per CU, every split >= 256 k.
+    // 64x64 tiles, WBK = 32; split K (the B*P reduction) over workgroups.
+    constexpr int WBK = 32;
+    const Device& d = device_info();
     const int64_t K = (int64_t)B * Ho * Wo;
-    const int64_t tiles = (int64_t)((Cin * KS * KS + 63) / 64) * ((Cout + 63) / 64);
-    int64_t want = (1024 + tiles - 1) / tiles;
-    int64_t maxs = (K + 255) / 256;
+    const int64_t Ntot = (int64_t)Cin * KS * KS;
+    const int64_t tiles = ((Ntot + 63) / 64) * ((Cout + 63) / 64);
+    const int64_t nsteps = (K + WBK - 1) / WBK;
+    int64_t maxs = (K + 255) / 256;                     // every split >= 256 k
     // keep the slab (splits * Cout * (Ntot+1) floats, written + re-read) no larger
     // than the operands it is computed from (dy and x: K * (Cout + Cin) floats)
-    const int64_t cap = (K * (Cout + Cin)) / ((int64_t)Cout * (Cin * KS * KS + 1));
+    const int64_t cap = (K * (Cout + Cin)) / ((int64_t)Cout * (Ntot + 1));
     if (maxs > cap) maxs = cap;
-    if (want > maxs) want = maxs;
-    if (want < 1) want = 1;
-    int64_t chunk = (K + want - 1) / want;
-    chunk = (chunk + 31) / 32 * 32;
+    if (maxs > 512) maxs = 512;
+    if (maxs < 1) maxs = 1;
+    const int s = best_split(tiles, nsteps, (int)maxs, d.occ_wgrad, d.ncu, 2.0 * 64 * 64 * WBK,
+                             4.0 * Cout * (Ntot + 1));
+    int64_t chunk = (K + s - 1) / s;
+    chunk = (chunk + WBK - 1) / WBK * WBK;
     *kchunk = (int)chunk;
     *splits = (int)((K + chunk - 1) / chunk);
+}
+
+const Device& device_info() {
+    static Device d = [] {
+        Device r;
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            r.ncu = v;
+        int o = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_fwd_kernel<128, 128, 3, 1, true, false, true>, NT,
+                                                         0) == hipSuccess && o > 0)
+            r.occ_fwd128 = o;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_fwd_kernel<64, 128, 3, 1, true, false, true>, NT,
+                                                         0) == hipSuccess && o > 0)
+            r.occ_fwd64 = o;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_wgrad_kernel<64, 64, 3, 1, true, true>, NT, 0) ==
+                hipSuccess && o > 0)
+            r.occ_wgrad = o;
+        (void)hipGetLastError();
+        return r;
+    }();
+    return d;
 }
 
 }  // namespace
