@@ -300,7 +300,27 @@ CONV_CASES = [
     (2, 17, 8, 256, 1, 1, False, True),      # merge_preds: Cin 17
     (2, 3, 64, 64, 7, 2, False, False),      # stem
     (1, 256, 2, 256, 3, 1, True, True),      # tiny spatial
+    (8, 128, 32, 128, 3, 1, True, False),    # split-K in every pass
+    (2, 64, 6, 32, 3, 1, True, False),       # Wo % 4 != 0: scalar wgrad path
+    (3, 32, 5, 48, 1, 1, True, True),        # P % 4 != 0: scalar wgrad path
 ]
+
+
+def test_conv_wgrad_misaligned_dy():
+    """dy at a 4-byte (not 16-byte) offset takes the scalar weight-gradient path."""
+    from ubpl_amd import kernels as Kn
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 64, 16, 16, generator=gen)
+    dy = torch.randn(2, 64, 16, 16, generator=gen)
+    w = torch.zeros(64, 64, 3, 3, requires_grad=True)
+    F.conv2d(x, w, None, 1, 1).backward(dy)
+    buf = torch.empty(dy.numel() + 1, device=DEV)
+    dyd = buf[1:].view_as(dy)
+    dyd.copy_(dy.to(DEV))
+    dw, db = torch.zeros(64, 64, 3, 3, device=DEV), torch.zeros(64, device=DEV)
+    Kn.conv2d_wgrad(dyd, x.to(DEV), 3, 1, dw, db, accumulate=False)
+    _close(dw, w.grad, rtol=1e-4, atol=1e-5 * float(w.grad.abs().max()))
+    _close(db, dy.sum((0, 2, 3)), rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("case", CONV_CASES)

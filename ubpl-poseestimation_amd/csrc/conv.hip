@@ -450,27 +450,272 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
     if (bias_blk && tid < BM && m0 + tid < Cout) sl[(int64_t)(m0 + tid) * Nt + Ntot] = bsum;
 }
 
+// component-wise select (a float4 ternary can be lowered to a pointer select through scratch)
+__device__ __forceinline__ float4 sel4(bool ok, float4 v) {
+    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+}
+
+// ------------------------------------------------------------------ wgrad v2
+// Both operands run along k = b*P + p in memory (dY[b][m][p], x[b][ci][p']),
+// so they are staged k-contiguous: float4 global loads, As[m][16] / Bs[n][16]
+// (64-B rows of four 16-B slots, slot XOR-swizzled by (row>>2)&3: conflict-free
+// ds_write_b128 and ds_read_b128, no padding, 32 KB double-buffered).  Inside
+// a 16-k step the reduction order is permuted: lane half h = l>>5 takes
+// k = 8h + 4q + e at MFMA (q, e), so one ds_read_b128 carries the operands of
+// four MFMAs.  n is tap-major (n = tap*Cin + ci) with the tap decoded per
+// staged row once, so any Cin (64, the stem's 3) works; the n-tile-0
+// workgroups sum their dY rows from registers (bias gradient).
+template <int BM, int BN, int KS, int ST, bool PRO, bool VEC1>
+__global__ void __launch_bounds__(NT, 4) conv_wgrad2_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                           const float* __restrict__ pscale,
+                                                           const float* __restrict__ pshift, int B, int Cin, int H,
+                                                           int W, int Cout, int Ho, int Wo, int kchunk,
+                                                           float* __restrict__ slab, int with_bias) {
+    constexpr int PADK = (KS - 1) / 2;
+    constexpr int TM = BM / 64, TN = BN / 64;
+    constexpr int AR = BM / 64, BR = BN / 64;   // staged rows per thread
+    __shared__ float4 As[2][BM * 4];
+    __shared__ float4 Bs[2][BN * 4];
+    __shared__ float s_sc[PRO ? MAXC : 1], s_sh[PRO ? MAXC : 1];
+
+    const int P = Ho * Wo, HWin = H * W;
+    const int Kall = B * P;
+    const int Ntot = Cin * KS * KS, Nt = Ntot + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
+    const int m0 = blockIdx.y * BM, nb0 = blockIdx.x * BN;
+    const int k_begin = blockIdx.z * kchunk;
+    const int k_end = min(Kall, k_begin + kchunk);
+    const int q = tid & 3, r0 = tid >> 2;
+    const bool bias_blk = with_bias && blockIdx.x == 0;
+
+    if (PRO) {
+        for (int c = tid; c < Cin; c += NT) {
+            s_sc[c] = pscale[c];
+            s_sh[c] = pshift[c];
+        }
+        __syncthreads();
+    }
+    int am[AR];
+    bool aok[AR];
+#pragma unroll
+    for (int j = 0; j < AR; ++j) {
+        const int m = m0 + r0 + 64 * j;
+        aok[j] = m < Cout;
+        am[j] = min(m, Cout - 1);
+    }
+    int bci[BR], bdh[BR], bdw[BR];
+    bool bok[BR];
+#pragma unroll
+    for (int j = 0; j < BR; ++j) {
+        const int n = nb0 + r0 + 64 * j;
+        bok[j] = n < Ntot;
+        const int nn = min(n, Ntot - 1);
+        const int tap = nn / Cin, ci = nn - tap * Cin;
+        const int kh = tap / KS, kw = tap - kh * KS;
+        bci[j] = ci;
+        bdh[j] = kh - PADK;
+        bdw[j] = kw - PADK;
+    }
+
+    float4 ra[AR], rb[BR];
+    float bsum[AR];
+#pragma unroll
+    for (int j = 0; j < AR; ++j) bsum[j] = 0.f;
+    auto load = [&](int kt) {
+        const int k = kt + 4 * q;
+        const bool kv = k < k_end;                  // k_end % 4 == 0: all four or none
+        const int kc = kv ? k : k_begin;
+        const int b = kc / P, p = kc - b * P;
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            const float4 v = *reinterpret_cast<const float4*>(dy + ((int64_t)b * Cout + am[j]) * P + p);
+            ra[j] = sel4(kv && aok[j], v);
+        }
+        if constexpr (VEC1) {
+#pragma unroll
+            for (int j = 0; j < BR; ++j) {
+                float4 v = *reinterpret_cast<const float4*>(x + ((int64_t)b * Cin + bci[j]) * HWin + p);
+                if (PRO) {
+                    const float sc = s_sc[bci[j]], sh = s_sh[bci[j]];
+                    v.x = fmaxf(fmaf(v.x, sc, sh), 0.f);
+                    v.y = fmaxf(fmaf(v.y, sc, sh), 0.f);
+                    v.z = fmaxf(fmaf(v.z, sc, sh), 0.f);
+                    v.w = fmaxf(fmaf(v.w, sc, sh), 0.f);
+                }
+                rb[j] = sel4(kv && bok[j], v);
+            }
+        } else {
+            const int oh = p / Wo, ow = p - oh * Wo;   // Wo % 4 == 0: one output row
+#pragma unroll
+            for (int j = 0; j < BR; ++j) {
+                const int ih = oh * ST + bdh[j];
+                const bool rok = kv && bok[j] && ih >= 0 && ih < H;
+                const float* src = x + ((int64_t)b * Cin + bci[j]) * HWin + (rok ? ih * W : 0);
+                const float sc = PRO ? s_sc[bci[j]] : 1.f, sh = PRO ? s_sh[bci[j]] : 0.f;
+                float e4[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int iw = (ow + e) * ST + bdw[j];
+                    const bool ok = rok && iw >= 0 && iw < W;
+                    float v = src[ok ? iw : 0];
+                    if (PRO) v = fmaxf(fmaf(v, sc, sh), 0.f);
+                    e4[e] = ok ? v : 0.f;
+                }
+                rb[j] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+            }
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            const int row = r0 + 64 * j;
+            As[buf][row * 4 + (q ^ ((row >> 2) & 3))] = ra[j];
+            if (bias_blk) bsum[j] += (ra[j].x + ra[j].y) + (ra[j].z + ra[j].w);
+        }
+#pragma unroll
+        for (int j = 0; j < BR; ++j) {
+            const int row = r0 + 64 * j;
+            Bs[buf][row * 4 + (q ^ ((row >> 2) & 3))] = rb[j];
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nkt = (k_end - k_begin + 15) / 16;
+    if (nkt > 0) {
+        load(k_begin);
+        store(0);
+    }
+    __syncthreads();
+    const int li = lane & 31, h = lane >> 5;
+    for (int t = 0; t < nkt; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < nkt) load(k_begin + (t + 1) * 16);
+#pragma unroll
+        for (int q2 = 0; q2 < 2; ++q2) {
+            const int sl = 2 * h + q2;
+            float4 af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int row = wm + 32 * i + li;
+                af[i] = As[cur][row * 4 + (sl ^ ((row >> 2) & 3))];
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int row = wn + 32 * j + li;
+                bf[j] = Bs[cur][row * 4 + (sl ^ ((row >> 2) & 3))];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
+        }
+        if (t + 1 < nkt) {
+            store(cur ^ 1);
+            __syncthreads();
+        }
+    }
+
+    float* sl = slab + (int64_t)blockIdx.z * Cout * Nt;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = nb0 + wn + 32 * j + li;
+        if (n >= Ntot) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < Cout) sl[(int64_t)m * Nt + n] = acc[i][j][r];
+            }
+    }
+    if (bias_blk) {
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            float v = bsum[j];
+            v += __shfl_xor(v, 1, 64);
+            v += __shfl_xor(v, 2, 64);
+            if (q == 0 && aok[j]) sl[(int64_t)(m0 + r0 + 64 * j) * Nt + Ntot] = v;
+        }
+    }
+}
+
 // slab columns are tap-major (n = tap*Cin + ci); dw is the reference layout
-// [Cout][Cin][KS][KS] (ci*KS*KS + tap).
+// [Cout][Cin][KS][KS] (ci*KS*KS + tap).  R split-lanes per output element
+// (256/R elements per block) sum interleaved splits with two accumulators;
+// the R partials are combined in a fixed order (deterministic).
+template <int R>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Cout,
                                                           int Cin, int T, int with_bias, float* __restrict__ dw,
                                                           float* __restrict__ db, int accumulate) {
+    constexpr int C = 256 / R;
+    __shared__ float red[R][C];
     const int Ntot = Cin * T;
     const int Nt = Ntot + 1;
     const int64_t total = (int64_t)Cout * Nt;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = threadIdx.x % C, r = threadIdx.x / C;
+    for (int64_t i0 = (int64_t)blockIdx.x * C; i0 < total; i0 += (int64_t)gridDim.x * C) {
+        const int64_t i = i0 + c;
+        const int64_t ic = i < total ? i : total - 1;
+        float s0 = 0.f, s1 = 0.f;
+        int z = r;
+        for (; z + R < splits; z += 2 * R) {
+            s0 += slab[(int64_t)z * total + ic];
+            s1 += slab[(int64_t)(z + R) * total + ic];
+        }
+        if (z < splits) s0 += slab[(int64_t)z * total + ic];
+        float s = s0 + s1;
+        if (R > 1) {
+            red[r][c] = s;
+            __syncthreads();
+            if (r == 0) {
+                s = red[0][c];
+#pragma unroll
+                for (int q = 1; q < R; ++q) s += red[q][c];
+            }
+            __syncthreads();
+        }
+        if (r != 0 || i >= total) continue;
         const int m = (int)(i / Nt), n = (int)(i - (int64_t)m * Nt);
-        if (n == Ntot && !with_bias) continue;
-        float s = 0.f;
-        for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * total + i];
         if (n < Ntot) {
             const int tap = n / Cin, ci = n - tap * Cin;
             float* d = dw + (int64_t)m * Ntot + (int64_t)ci * T + tap;
             *d = accumulate ? *d + s : s;
-        } else if (db) {
+        } else if (with_bias && db) {
             db[m] = accumulate ? db[m] + s : s;
         }
     }
+}
+
+int launch_wgrad_reduce(const float* slab, int splits, int Cout, int Cin, int T, int wb, float* dw, float* db,
+                        int accumulate, hipStream_t st) {
+    const int64_t total = (int64_t)Cout * (Cin * T + 1);
+    int R = 1;
+    while (R < 16 && R * 32 < splits) R *= 2;           // <= ~32 loads per thread
+    const int C = 256 / R;
+    int64_t g = (total + C - 1) / C;
+    if (g > 8192) g = 8192;
+    switch (R) {
+#define UBPL_RED(R_)                                                                                                 \
+    case R_:                                                                                                         \
+        hipLaunchKernelGGL(wgrad_reduce_kernel<R_>, dim3((unsigned)g), dim3(256), 0, st, slab, splits, Cout, Cin, T, \
+                           wb, dw, db, accumulate);                                                                  \
+        break;
+        UBPL_RED(1) UBPL_RED(2) UBPL_RED(4) UBPL_RED(8) UBPL_RED(16)
+#undef UBPL_RED
+    }
+    UBPL_LAUNCH_CHECK();
+    return 0;
 }
 
 // wt[co][tap][ci] = w[co][ci][tap]
@@ -536,6 +781,7 @@ struct Plan {
 struct Device {
     int ncu = 256;
     int occ_fwd128 = 4, occ_fwd64 = 5, occ_wgrad = 4;
+    int occ_w2[2][2] = {{8, 5}, {5, 4}};   // [bm == 128][bn == 128]
 };
 
 const Device& device_info();
@@ -625,6 +871,29 @@ int fwd_bm(const Plan& pl, const float* x, const float* w, const float* bias, co
                                                        slab, st);
 }
 
+template <int BM, int BN, int KS, int ST, bool PRO, bool VEC1>
+int wgrad2_launch(const float* dy, const float* x, const float* ps, const float* sh, int B, int Cin, int H, int W,
+                  int Cout, int Ho, int Wo, int splits, int kchunk, float* slab, int with_bias, hipStream_t st) {
+    const int Ntot = Cin * KS * KS;
+    dim3 grid((unsigned)((Ntot + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM), (unsigned)splits);
+    hipLaunchKernelGGL((conv_wgrad2_kernel<BM, BN, KS, ST, PRO, VEC1>), grid, dim3(NT), 0, st, dy, x, ps, sh, B, Cin,
+                       H, W, Cout, Ho, Wo, kchunk, slab, with_bias);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+template <int KS, int ST, bool PRO, bool VEC1>
+int wgrad2_tile(int bm, int bn, const float* dy, const float* x, const float* ps, const float* sh, int B, int Cin,
+                int H, int W, int Cout, int Ho, int Wo, int splits, int kchunk, float* slab, int wb, hipStream_t st) {
+    if (bm == 128 && bn == 128)
+        return wgrad2_launch<128, 128, KS, ST, PRO, VEC1>(dy, x, ps, sh, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+    if (bm == 128)
+        return wgrad2_launch<128, 64, KS, ST, PRO, VEC1>(dy, x, ps, sh, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+    if (bn == 128)
+        return wgrad2_launch<64, 128, KS, ST, PRO, VEC1>(dy, x, ps, sh, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+    return wgrad2_launch<64, 64, KS, ST, PRO, VEC1>(dy, x, ps, sh, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+}
+
 template <int KS, int ST, bool PRO, bool TAPN>
 int wgrad_launch(const float* dy, const float* x, const float* ps, const float* sh, int B, int Cin, int H, int W,
                  int Cout, int Ho, int Wo, int splits, int kchunk, float* slab, int with_bias, hipStream_t st) {
@@ -637,27 +906,57 @@ int wgrad_launch(const float* dy, const float* x, const float* ps, const float* 
     return 0;
 }
 
-void wgrad_plan(int B, int Cin, int Cout, int KS, int Ho, int Wo, int* splits, int* kchunk) {
-    // 64x64 tiles, WBK = 32; split K (the B*P reduction) over workgroups.
-    constexpr int WBK = 32;
+// k-contiguous float4 staging (conv_wgrad2_kernel) needs P % 4 == 0 and, for a
+// spatial kernel, whole float4 groups inside one output row.
+bool wgrad_v2_shape(int KS, int Ho, int Wo) { return (Ho * Wo) % 4 == 0 && (KS == 1 || Wo % 4 == 0); }
+
+struct WPlan {
+    int splits, kchunk, bm, bn;
+};
+
+// Split of the k = b*P + p reduction over workgroups for the weight gradient.
+// v2: BM x BN tiles in {64,128}^2, 16-k steps, chosen by the cost model with a
+// per-flop efficiency for the smaller tiles; v1: 64x64, 32-k steps.
+WPlan wgrad_plan(int B, int Cin, int Cout, int KS, int Ho, int Wo, bool v2) {
     const Device& d = device_info();
     const int64_t K = (int64_t)B * Ho * Wo;
     const int64_t Ntot = (int64_t)Cin * KS * KS;
-    const int64_t tiles = ((Ntot + 63) / 64) * ((Cout + 63) / 64);
-    const int64_t nsteps = (K + WBK - 1) / WBK;
-    int64_t maxs = (K + 255) / 256;                     // every split >= 256 k
     // keep the slab (splits * Cout * (Ntot+1) floats, written + re-read) no larger
     // than the operands it is computed from (dy and x: K * (Cout + Cin) floats)
-    const int64_t cap = (K * (Cout + Cin)) / ((int64_t)Cout * (Ntot + 1));
-    if (maxs > cap) maxs = cap;
-    if (maxs > 512) maxs = 512;
-    if (maxs < 1) maxs = 1;
-    const int s = best_split(tiles, nsteps, (int)maxs, d.occ_wgrad, d.ncu, 2.0 * 64 * 64 * WBK,
-                             4.0 * Cout * (Ntot + 1));
-    int64_t chunk = (K + s - 1) / s;
-    chunk = (chunk + WBK - 1) / WBK * WBK;
-    *kchunk = (int)chunk;
-    *splits = (int)((K + chunk - 1) / chunk);
+    // (slabs up to 8 MB are allowed regardless: small levels need the splits)
+    int64_t cap = (K * (Cout + Cin)) / ((int64_t)Cout * (Ntot + 1));
+    const int64_t cap_small = (int64_t)(8 << 20) / (4 * (int64_t)Cout * (Ntot + 1));
+    if (cap < cap_small) cap = cap_small;
+    WPlan best{1, 0, 64, 64};
+    double bc = 1e30;
+    for (int bm : {128, 64})
+        for (int bn : {128, 64}) {
+            if (!v2 && (bm != 64 || bn != 64)) continue;
+            if (bm == 128 && Cout <= 64) continue;
+            if (bn == 128 && Ntot <= 64) continue;
+            const int kb = v2 ? 16 : 32;
+            const int64_t tiles = ((Ntot + bn - 1) / bn) * ((Cout + bm - 1) / bm);
+            const int64_t nsteps = (K + kb - 1) / kb;
+            int64_t maxs = (K + 4 * kb - 1) / (4 * kb);     // every split >= 4 k steps
+            if (maxs > cap) maxs = cap;
+            if (maxs > 512) maxs = 512;
+            if (maxs < 1) maxs = 1;
+            const int occ = v2 ? d.occ_w2[bm == 128][bn == 128] : d.occ_wgrad;
+            const double sf = 2.0 * bm * bn * kb, sb = 4.0 * Cout * (Ntot + 1);
+            const int s = best_split(tiles, nsteps, (int)maxs, occ, d.ncu, sf, sb);
+            const double eff = (bm * bn == 16384) ? 1.0 : (bm * bn == 8192 ? 0.85 : 0.7);
+            const double c = split_cost(tiles, s, nsteps, occ, d.ncu, sf, sb) / eff;
+            if (c < bc) {
+                bc = c;
+                int64_t chunk = (K + s - 1) / s;
+                chunk = (chunk + kb - 1) / kb * kb;
+                best.kchunk = (int)chunk;
+                best.splits = (int)((K + chunk - 1) / chunk);
+                best.bm = bm;
+                best.bn = bn;
+            }
+        }
+    return best;
 }
 
 const Device& device_info() {
@@ -677,6 +976,14 @@ const Device& device_info() {
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_wgrad_kernel<64, 64, 3, 1, true, true>, NT, 0) ==
                 hipSuccess && o > 0)
             r.occ_wgrad = o;
+        auto q = [&](const void* f, int& dst) {
+            int v2 = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v2, f, NT, 0) == hipSuccess && v2 > 0) dst = v2;
+        };
+        q((const void*)conv_wgrad2_kernel<64, 64, 3, 1, true, false>, r.occ_w2[0][0]);
+        q((const void*)conv_wgrad2_kernel<64, 128, 3, 1, true, false>, r.occ_w2[0][1]);
+        q((const void*)conv_wgrad2_kernel<128, 64, 3, 1, true, false>, r.occ_w2[1][0]);
+        q((const void*)conv_wgrad2_kernel<128, 128, 3, 1, true, false>, r.occ_w2[1][1]);
         (void)hipGetLastError();
         return r;
     }();
@@ -728,9 +1035,12 @@ UBPL_API int ubpl_conv2d_forward(const float* x, int B, int Cin, int H, int W, c
 
 // Floats of slab workspace ubpl_conv2d_wgrad needs.
 UBPL_API int64_t ubpl_conv2d_wgrad_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo) {
-    int splits, kchunk;
-    wgrad_plan(B, Cin, Cout, KS, Ho, Wo, &splits, &kchunk);
-    return (int64_t)splits * Cout * (Cin * KS * KS + 1);
+    int64_t s = wgrad_plan(B, Cin, Cout, KS, Ho, Wo, false).splits;
+    if (wgrad_v2_shape(KS, Ho, Wo)) {
+        const int64_t s2 = wgrad_plan(B, Cin, Cout, KS, Ho, Wo, true).splits;
+        if (s2 > s) s = s2;
+    }
+    return s * Cout * (Cin * KS * KS + 1);
 }
 
 // dw[Cout,Cin,KS,KS] (+)= sum over (b,p) dy * im2col(relu(x*pscale+pshift) or x);
@@ -740,34 +1050,47 @@ UBPL_API int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, 
                                float* dw, float* db, int accumulate, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (pscale != nullptr && Cin > MAXC) return (int)hipErrorInvalidValue;
-    int splits, kchunk;
-    wgrad_plan(B, Cin, Cout, KS, Ho, Wo, &splits, &kchunk);
     const bool pro = pscale != nullptr;
     const int wb = db != nullptr;
-    const bool tapn = (KS == 1) || (Cin % 64 == 0);
+    const bool v2 = wgrad_v2_shape(KS, Ho, Wo) && (((uintptr_t)dy & 15) == 0);
+    const WPlan pl = wgrad_plan(B, Cin, Cout, KS, Ho, Wo, v2);
+    const int splits = pl.splits, kchunk = pl.kchunk;
     int rc;
-    if (KS == 1 && stride == 1)
-        rc = pro ? wgrad_launch<1, 1, true, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
-                 : wgrad_launch<1, 1, false, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
-    else if (KS == 3 && stride == 1 && tapn)
-        rc = pro ? wgrad_launch<3, 1, true, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
-                 : wgrad_launch<3, 1, false, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
-    else if (KS == 3 && stride == 1)
-        rc = pro ? wgrad_launch<3, 1, true, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
-                 : wgrad_launch<3, 1, false, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
-    else if (KS == 7 && stride == 2)
-        rc = pro ? wgrad_launch<7, 2, true, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
-                 : wgrad_launch<7, 2, false, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
-    else
-        return (int)hipErrorInvalidValue;
+    if (v2) {
+        const bool vec1 = KS == 1 && stride == 1 && (((uintptr_t)x & 15) == 0) && ((H * W) % 4 == 0);
+#define UBPL_W2(KS_, ST_, VEC_)                                                                                     \
+    (pro ? wgrad2_tile<KS_, ST_, true, VEC_>(pl.bm, pl.bn, dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits,  \
+                                             kchunk, slab, wb, st)                                                    \
+         : wgrad2_tile<KS_, ST_, false, VEC_>(pl.bm, pl.bn, dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, \
+                                              kchunk, slab, wb, st))
+        if (KS == 1 && stride == 1)
+            rc = vec1 ? UBPL_W2(1, 1, true) : UBPL_W2(1, 1, false);
+        else if (KS == 3 && stride == 1)
+            rc = UBPL_W2(3, 1, false);
+        else if (KS == 7 && stride == 2)
+            rc = UBPL_W2(7, 2, false);
+        else
+            return (int)hipErrorInvalidValue;
+#undef UBPL_W2
+    } else {
+        const bool tapn = (KS == 1) || (Cin % 64 == 0);
+        if (KS == 1 && stride == 1)
+            rc = pro ? wgrad_launch<1, 1, true, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
+                     : wgrad_launch<1, 1, false, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+        else if (KS == 3 && stride == 1 && tapn)
+            rc = pro ? wgrad_launch<3, 1, true, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
+                     : wgrad_launch<3, 1, false, true>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+        else if (KS == 3 && stride == 1)
+            rc = pro ? wgrad_launch<3, 1, true, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
+                     : wgrad_launch<3, 1, false, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+        else if (KS == 7 && stride == 2)
+            rc = pro ? wgrad_launch<7, 2, true, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st)
+                     : wgrad_launch<7, 2, false, false>(dy, x, pscale, pshift, B, Cin, H, W, Cout, Ho, Wo, splits, kchunk, slab, wb, st);
+        else
+            return (int)hipErrorInvalidValue;
+    }
     if (rc) return rc;
-    const int64_t total = (int64_t)Cout * (Cin * KS * KS + 1);
-    int grid = (int)((total + 255) / 256);
-    if (grid > 4096) grid = 4096;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, st, slab, splits, Cout, Cin, KS * KS, wb, dw, db,
-                       accumulate);
-    UBPL_LAUNCH_CHECK();
-    return 0;
+    return launch_wgrad_reduce(slab, splits, Cout, Cin, KS * KS, wb, dw, db, accumulate, st);
 }
 
 // Forward weight layout for KS > 1: wt[co][tap][ci] = w[co][ci][tap].
