@@ -109,9 +109,24 @@ class ConvTimer:
         flops_per_launch = self.flops / n
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
         return {"bound": "mfma", "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": (pmc_traffic() or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc_traffic(),
                 "kernel": "conv_fwd_kernel<3x3,f32 MFMA> (Residual conv2)", "launches": n,
                 "avg_launch_us": round(avg_ms * 1e3, 2), "flops_per_launch": int(flops_per_launch)}
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel, measured by rocprofv3 --pmc
+    passes over this bench command (tools/gpu_pmc.sh bench ->
+    tools/pmc_roofline.py -> profiles/pmc_roofline.json); None if absent."""
+    p = os.path.join(ROOT, "profiles", "pmc_roofline.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as fh:
+        d = json.load(fh)
+    return {"hbm_bytes_per_launch": int(d["hbm_bytes_per_launch"]),
+            "fetch_bytes_per_launch": int(d["fetch_bytes_per_launch"]),
+            "write_bytes_per_launch": int(d["write_bytes_per_launch"]), "source": d.get("source")}
 
 
 def cpu_baseline(steps=2, B=4):

@@ -83,9 +83,12 @@ int ubpl_scale_(float* x, int64_t n, float s, void* stream);
 
 /* ---------------------------------------------------------------- H2-H4 --
  * BatchNorm2d (models/base/layers.py:41,57-61), train-mode statistics.
- * part: scratch of 2*C*ubpl_bn_splits(B,C) doubles.  rmean/rvar updated with
- * momentum (nullable).  scale = gamma*invstd, shift = beta - mean*scale. */
+ * part: scratch of ubpl_bn_part_doubles(B,C) doubles, ZEROED before its first
+ * use (arrival counters for C <= 512 channels at its head, which each call
+ * leaves at zero, then the partial sums; one call at a time per scratch).  rmean/rvar updated with momentum
+ * (nullable).  scale = gamma*invstd, shift = beta - mean*scale. */
 int ubpl_bn_splits(int B, int C);
+int64_t ubpl_bn_part_doubles(int B, int C);
 int ubpl_bn_forward_stats(const float* x, int B, int C, int HW, const float* gamma, const float* beta, float eps,
                           float momentum, float* rmean, float* rvar, double* part, float* mean_out,
                           float* invstd_out, float* scale, float* shift, void* stream);
@@ -101,8 +104,10 @@ int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, cons
 
 /* Conv (models/base/layers.py:31-50): 1x1/s1, 3x3/s1, 7x7/s2, pad (KS-1)/2,
  * optional fused pre-activation relu(x*pscale + pshift), bias, residual add
- * (res may alias y).  MFMA f32 implicit GEMM, tap-major K (k = tap*Cin + ci):
- * for KS > 1 the weights must be in the layout ubpl_conv_weight_tapmajor makes.
+ * (res may alias y).  MFMA f32 implicit GEMM over a grouped tap-major K,
+ * k = (ci/G)*G*T + tap*G + ci%G (T = KS*KS, G = 16 if 16 | Cin else Cin):
+ * for KS > 1 the weights must be in the layout ubpl_conv_weight_tapmajor makes,
+ * [Cout][Cin/G][T][G] (for KS == 1 that is the reference layout itself).
  * Small grids split K over workgroups: slab = ubpl_conv2d_forward_workspace
  * floats (nullable when that is 0). */
 int64_t ubpl_conv2d_forward_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo);
@@ -115,8 +120,9 @@ int64_t ubpl_conv2d_wgrad_workspace(int B, int Cin, int Cout, int KS, int Ho, in
 int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, int H, int W, int Cout, int KS, int stride,
                       const float* pscale, const float* pshift, int Ho, int Wo, float* slab, float* dw, float* db,
                       int accumulate, void* stream);
-/* Data-gradient weights (stride 1): the tap-major layout of the flipped,
- * transposed kernel, so dx = ubpl_conv2d_forward(dy, wt). */
+/* Data-gradient weights (stride 1): the forward layout of the flipped,
+ * transposed kernel ([Cin][Cout/G][T][G], G from Cout), so
+ * dx = ubpl_conv2d_forward(dy, wt). */
 int ubpl_conv_weight_flip(const float* w, int Cout, int Cin, int KS, float* wt, void* stream);
 /* Both re-layouts for many convs in one launch: table int64 [nseg][5] =
  * (src_off, dst_off, Cout, Cin, KS*KS) in floats; mode 0 tap-major, 1 dgrad. */

@@ -241,7 +241,7 @@ def test_bn_forward_backward_vs_torch():
         y = F.relu(F.batch_norm(xr, rmr, rvr, gr, br, True, 0.1, 1e-5))
         y.backward(dz)
         xd = x.to(DEV)
-        part = torch.empty(2 * C * Kn.bn_splits(B, C), dtype=torch.float64, device=DEV)
+        part = Kn.bn_part(B, C, DEV)
         mean, istd, sc, sh = [torch.empty(C, device=DEV) for _ in range(4)]
         rmd, rvd = rm.to(DEV), rv.to(DEV)
         Kn.bn_forward_stats(xd, gam.to(DEV), bet.to(DEV), 1e-5, 0.1, rmd, rvd, part, mean, istd, sc, sh)

@@ -1,0 +1,51 @@
+"""HBM traffic per launch of bench.py's roofline kernel, from rocprofv3 --pmc
+passes over the bench command itself (tools/gpu_pmc.sh, mode "bench").
+
+The roofline kernel is every 3x3 forward conv with the fused BN prologue
+(conv_fwd_kernel<BM, 128, 3, 1, PRO=true, ...>, both tile heights), as in
+bench.py's ConvTimer.  Bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are KiB; gfx950's FETCH_SIZE counts half the bytes of wide reads,
+so it is doubled.  Writes profiles/pmc_roofline.json for bench.py.
+
+    python tools/pmc_roofline.py gpurun_out/pmc_bench profiles/pmc_roofline.json [source-tag]
+"""
+import csv
+import json
+import os
+import re
+import sys
+
+PAT = re.compile(r"conv_fwd_kernel<(\d+), 128, 3, 1, true, false")
+
+
+def per_launch(path, counter):
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter or not PAT.search(r["Kernel_Name"]):
+            continue
+        vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return vals
+
+
+def main():
+    d = sys.argv[1]
+    out = sys.argv[2]
+    tag = sys.argv[3] if len(sys.argv) > 3 else d
+    fetch = per_launch(os.path.join(d, "fetch_counter_collection.csv"), "FETCH_SIZE")
+    write = per_launch(os.path.join(d, "write_counter_collection.csv"), "WRITE_SIZE")
+    nf, nw = len(fetch), len(write)
+    fb = 2 * 1024 * sum(fetch.values()) / max(nf, 1)
+    wb = 1024 * sum(write.values()) / max(nw, 1)
+    res = {"kernel": "conv_fwd_kernel<*,128,3,1,PRO> (all launches of the bench step)",
+           "launches_fetch_pass": nf, "launches_write_pass": nw,
+           "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+           "hbm_bytes_per_launch": fb + wb,
+           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over bench.py; FETCH_SIZE x2 (gfx950)",
+           "source": tag}
+    print(json.dumps(res, indent=1))
+    with open(out, "w") as fh:
+        fh.write(json.dumps(res, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -9,8 +9,9 @@
 //
 // Statistics: each (channel, batch-slice) workgroup accumulates sum and sum of
 // squares of (x - x0) — x0 a sample of the channel, which removes the
-// cancellation of E[x^2] - E[x]^2 — then reduces in f64.  Partials are written
-// to a slab and combined by a finalize kernel: deterministic, no atomics.
+// cancellation of E[x^2] - E[x]^2 — then reduces in f64.  Partials go to a
+// slab; the channel's last-arriving workgroup (ticket counter) combines them
+// in slice order: deterministic, one launch.
 //
 // Backward: dyp = dz * [x*scale + shift > 0] (ReLU mask recomputed bit-for-bit
 // as the forward prologue computed it); per channel S1 = sum dyp,
@@ -21,69 +22,98 @@
 
 namespace {
 
+// Last-arriver hand-off (cdna_hip_programming.md §6 Guideline 16, split-K
+// counter form with write-through payload): thread 0 of every (channel,
+// slice) block stores its two partials with agent-scope atomic stores (sc1,
+// write-through: no release fence, which would write back the whole L2),
+// drains them, and takes a ticket; the block drawing the last ticket reads the
+// channel's partials with agent-scope atomic loads (sc1: past any stale L1
+// line) in slice order (deterministic) and resets the counter.
+__device__ __forceinline__ void publish2(double* p, double a, double b) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(a),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p + 1), (unsigned long long)__double_as_longlong(b),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ double consume(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__device__ __forceinline__ bool last_arriver(unsigned* cnt, unsigned n) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old != n - 1) return false;
+    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+struct StatsOut {
+    const float* gamma;
+    const float* beta;
+    float eps, momentum;
+    float *rmean, *rvar, *mean_out, *invstd_out, *scale, *shift;
+};
+
+// One (channel c, batch slice) per block over the flattened (b, pixel) range:
+// sum and sum of squares of (x - x0), x0 = x[0, c, 0]; f32 per thread, f64
+// across the block and the slices.  The last block of channel c finalizes it.
 template <bool VEC>
-__global__ void __launch_bounds__(256) stats_partial_kernel(const float* __restrict__ x, int B, int C, int HW,
-                                                           int bper, double* __restrict__ part) {
+__global__ void __launch_bounds__(256) stats_kernel(const float* __restrict__ x, int B, int C, int HW, int bper,
+                                                   double* __restrict__ part, unsigned* __restrict__ cnt,
+                                                   StatsOut o) {
     __shared__ double red[16];
     const int c = blockIdx.x, sp = blockIdx.y;
     const int b0 = sp * bper, b1 = min(B, b0 + bper);
     const float x0 = x[(int64_t)c * HW];
     float s1 = 0.f, s2 = 0.f;
-    for (int b = b0; b < b1; ++b) {
-        const float* p = x + ((int64_t)b * C + c) * HW;
-        if (VEC) {
-            const float4* p4 = reinterpret_cast<const float4*>(p);
-            for (int i = threadIdx.x; i < (HW >> 2); i += blockDim.x) {
-                const float4 v = p4[i];
-                const float a = v.x - x0, bb = v.y - x0, cc = v.z - x0, d = v.w - x0;
-                s1 += (a + bb) + (cc + d);
-                s2 = fmaf(a, a, fmaf(bb, bb, fmaf(cc, cc, fmaf(d, d, s2))));
-            }
-        } else {
-            for (int i = threadIdx.x; i < HW; i += blockDim.x) {
-                const float a = p[i] - x0;
-                s1 += a;
-                s2 = fmaf(a, a, s2);
-            }
+    if (VEC) {
+        const int hw4 = HW >> 2;
+        const int n4 = (b1 - b0) * hw4;
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+        for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+            const int bb = i / hw4, o4 = i - bb * hw4;
+            const float4 v = x4[((int64_t)(b0 + bb) * C + c) * hw4 + o4];
+            const float a = v.x - x0, q = v.y - x0, r = v.z - x0, d = v.w - x0;
+            s1 += (a + q) + (r + d);
+            s2 = fmaf(a, a, fmaf(q, q, fmaf(r, r, fmaf(d, d, s2))));
+        }
+    } else {
+        const int n = (b1 - b0) * HW;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int bb = i / HW, o1 = i - bb * HW;
+            const float a = x[((int64_t)(b0 + bb) * C + c) * HW + o1] - x0;
+            s1 += a;
+            s2 = fmaf(a, a, s2);
         }
     }
     const double d1 = ubpl::block_sum((double)s1, red);
     const double d2 = ubpl::block_sum((double)s2, red);
-    if (threadIdx.x == 0) {
-        part[((int64_t)c * gridDim.y + sp) * 2 + 0] = d1;
-        part[((int64_t)c * gridDim.y + sp) * 2 + 1] = d2;
+    if (threadIdx.x != 0) return;
+    double* pc = part + (int64_t)c * gridDim.y * 2;
+    publish2(pc + sp * 2, d1, d2);
+    if (!last_arriver(cnt + c, gridDim.y)) return;
+    double t1 = 0.0, t2 = 0.0;
+    for (int q = 0; q < (int)gridDim.y; ++q) {
+        t1 += consume(pc + q * 2);
+        t2 += consume(pc + q * 2 + 1);
     }
-}
-
-__global__ void stats_finalize_kernel(const float* __restrict__ x, const double* __restrict__ part, int C, int HW,
-                                      int splits, int64_t N, const float* __restrict__ gamma,
-                                      const float* __restrict__ beta, float eps, float momentum,
-                                      float* __restrict__ rmean, float* __restrict__ rvar,
-                                      float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                                      float* __restrict__ scale, float* __restrict__ shift) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s1 = 0.0, s2 = 0.0;
-    for (int s = 0; s < splits; ++s) {
-        s1 += part[((int64_t)c * splits + s) * 2 + 0];
-        s2 += part[((int64_t)c * splits + s) * 2 + 1];
-    }
-    const double x0 = (double)x[(int64_t)c * HW];
-    const double m1 = s1 / (double)N;
-    double var = s2 / (double)N - m1 * m1;
+    const int64_t N = (int64_t)B * HW;
+    const double m1 = t1 / (double)N;
+    double var = t2 / (double)N - m1 * m1;
     if (var < 0) var = 0;
-    const double mean = x0 + m1;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float g = gamma[c];
-    const float sc = invstd * g;
-    mean_out[c] = (float)mean;
-    invstd_out[c] = invstd;
-    scale[c] = sc;
-    shift[c] = beta[c] - (float)mean * sc;
-    if (rmean) {
+    const double mean = (double)x0 + m1;
+    const float invstd = (float)(1.0 / sqrt(var + (double)o.eps));
+    const float sc = invstd * o.gamma[c];
+    o.mean_out[c] = (float)mean;
+    o.invstd_out[c] = invstd;
+    o.scale[c] = sc;
+    o.shift[c] = o.beta[c] - (float)mean * sc;
+    if (o.rmean) {
         const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
-        rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
-        rvar[c] = (float)((double)momentum * unb + (1.0 - (double)momentum) * (double)rvar[c]);
+        o.rmean[c] = (float)((double)o.momentum * mean + (1.0 - (double)o.momentum) * (double)o.rmean[c]);
+        o.rvar[c] = (float)((double)o.momentum * unb + (1.0 - (double)o.momentum) * (double)o.rvar[c]);
     }
 }
 
@@ -121,70 +151,77 @@ __global__ void __launch_bounds__(256) apply_kernel(const float* __restrict__ x,
     }
 }
 
+struct BwdOut {
+    const float* gamma;
+    const float* invstd;
+    float *dgamma, *dbeta, *ca, *cb, *cc;
+};
+
+// Per (channel, slice): S1 = sum dyp, S2 = sum dyp*(x - mean) with the ReLU
+// mask recomputed; the channel's last block produces dgamma/dbeta and the
+// coefficients of dx = a*dyp + b*(x - mean) + c.
 template <bool VEC>
-__global__ void __launch_bounds__(256) bwd_partial_kernel(const float* __restrict__ dz, const float* __restrict__ x,
-                                                         int B, int C, int HW, int bper,
-                                                         const float* __restrict__ scale,
-                                                         const float* __restrict__ shift,
-                                                         const float* __restrict__ mean, int relu,
-                                                         double* __restrict__ part) {
+__global__ void __launch_bounds__(256) bwd_stats_kernel(const float* __restrict__ dz, const float* __restrict__ x,
+                                                       int B, int C, int HW, int bper,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float* __restrict__ mean, int relu,
+                                                       double* __restrict__ part, unsigned* __restrict__ cnt,
+                                                       BwdOut o) {
     __shared__ double red[16];
     const int c = blockIdx.x, sp = blockIdx.y;
     const int b0 = sp * bper, b1 = min(B, b0 + bper);
     const float sc = scale[c], sh = shift[c], mu = mean[c];
     float s1 = 0.f, s2 = 0.f;
-    for (int b = b0; b < b1; ++b) {
-        const int64_t off = ((int64_t)b * C + c) * HW;
-        if (VEC) {
-            const float4* x4 = reinterpret_cast<const float4*>(x + off);
-            const float4* d4 = reinterpret_cast<const float4*>(dz + off);
-            for (int i = threadIdx.x; i < (HW >> 2); i += blockDim.x) {
-                const float4 xv = x4[i];
-                float4 g = d4[i];
-                if (relu) {
-                    g.x = fmaf(xv.x, sc, sh) > 0.f ? g.x : 0.f;
-                    g.y = fmaf(xv.y, sc, sh) > 0.f ? g.y : 0.f;
-                    g.z = fmaf(xv.z, sc, sh) > 0.f ? g.z : 0.f;
-                    g.w = fmaf(xv.w, sc, sh) > 0.f ? g.w : 0.f;
-                }
-                s1 += (g.x + g.y) + (g.z + g.w);
-                s2 = fmaf(g.x, xv.x - mu, fmaf(g.y, xv.y - mu, fmaf(g.z, xv.z - mu, fmaf(g.w, xv.w - mu, s2))));
+    if (VEC) {
+        const int hw4 = HW >> 2;
+        const int n4 = (b1 - b0) * hw4;
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+        const float4* d4 = reinterpret_cast<const float4*>(dz);
+        for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+            const int bb = i / hw4, o4 = i - bb * hw4;
+            const int64_t off = ((int64_t)(b0 + bb) * C + c) * hw4 + o4;
+            const float4 xv = x4[off];
+            float4 g = d4[off];
+            if (relu) {
+                g.x = fmaf(xv.x, sc, sh) > 0.f ? g.x : 0.f;
+                g.y = fmaf(xv.y, sc, sh) > 0.f ? g.y : 0.f;
+                g.z = fmaf(xv.z, sc, sh) > 0.f ? g.z : 0.f;
+                g.w = fmaf(xv.w, sc, sh) > 0.f ? g.w : 0.f;
             }
-        } else {
-            for (int i = threadIdx.x; i < HW; i += blockDim.x) {
-                const float xv = x[off + i];
-                float g = dz[off + i];
-                if (relu && !(fmaf(xv, sc, sh) > 0.f)) g = 0.f;
-                s1 += g;
-                s2 = fmaf(g, xv - mu, s2);
-            }
+            s1 += (g.x + g.y) + (g.z + g.w);
+            s2 = fmaf(g.x, xv.x - mu, fmaf(g.y, xv.y - mu, fmaf(g.z, xv.z - mu, fmaf(g.w, xv.w - mu, s2))));
+        }
+    } else {
+        const int n = (b1 - b0) * HW;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int bb = i / HW, o1 = i - bb * HW;
+            const int64_t off = ((int64_t)(b0 + bb) * C + c) * HW + o1;
+            const float xv = x[off];
+            float g = dz[off];
+            if (relu && !(fmaf(xv, sc, sh) > 0.f)) g = 0.f;
+            s1 += g;
+            s2 = fmaf(g, xv - mu, s2);
         }
     }
     const double d1 = ubpl::block_sum((double)s1, red);
     const double d2 = ubpl::block_sum((double)s2, red);
-    if (threadIdx.x == 0) {
-        part[((int64_t)c * gridDim.y + sp) * 2 + 0] = d1;
-        part[((int64_t)c * gridDim.y + sp) * 2 + 1] = d2;
+    if (threadIdx.x != 0) return;
+    double* pc = part + (int64_t)c * gridDim.y * 2;
+    publish2(pc + sp * 2, d1, d2);
+    if (!last_arriver(cnt + c, gridDim.y)) return;
+    double t1 = 0.0, t2 = 0.0;
+    for (int q = 0; q < (int)gridDim.y; ++q) {
+        t1 += consume(pc + q * 2);
+        t2 += consume(pc + q * 2 + 1);
     }
-}
-
-__global__ void bwd_finalize_kernel(const double* __restrict__ part, int C, int splits, int64_t N,
-                                    const float* __restrict__ gamma, const float* __restrict__ invstd,
-                                    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ ca,
-                                    float* __restrict__ cb, float* __restrict__ cc) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s1 = 0.0, s2 = 0.0;
-    for (int s = 0; s < splits; ++s) {
-        s1 += part[((int64_t)c * splits + s) * 2 + 0];
-        s2 += part[((int64_t)c * splits + s) * 2 + 1];
-    }
-    const double is = invstd[c], g = gamma[c];
-    if (dgamma) dgamma[c] += (float)(s2 * is);
-    if (dbeta) dbeta[c] += (float)s1;
-    ca[c] = (float)(g * is);
-    cb[c] = (float)(-g * is * is * is * s2 / (double)N);
-    cc[c] = (float)(-g * is * s1 / (double)N);
+    const double N = (double)((int64_t)B * HW);
+    const double is = o.invstd[c], g = o.gamma[c];
+    if (o.dgamma) o.dgamma[c] += (float)(t2 * is);
+    if (o.dbeta) o.dbeta[c] += (float)t1;
+    o.ca[c] = (float)(g * is);
+    o.cb[c] = (float)(-g * is * is * is * t2 / N);
+    o.cc[c] = (float)(-g * is * t1 / N);
 }
 
 __device__ __forceinline__ float bwd_one(float g, float xv, float sc, float sh, float mu, float a, float b, float c,
@@ -258,8 +295,14 @@ int grid_ew(int64_t n) {
 
 }  // namespace
 
-// Scratch: part must hold C * ubpl_bn_splits(B, C) * 2 doubles.
+// Scratch: part must hold ubpl_bn_part_doubles(B, C) doubles, ZEROED before
+// first use: MAXBN arrival counters at its head (a fixed place, whatever C a
+// call has; every call leaves them at zero again), then 2 * C * splits
+// partial sums.
+constexpr int MAXBN = 512;
+constexpr int CNT_DOUBLES = MAXBN / 2;
 UBPL_API int ubpl_bn_splits(int B, int C) { return splits_for(B, C); }
+UBPL_API int64_t ubpl_bn_part_doubles(int B, int C) { return CNT_DOUBLES + 2 * (int64_t)C * splits_for(B, C); }
 
 // Train-mode statistics of x [B,C,H,W] -> mean, invstd, (scale, shift) and the
 // running-stat update (rmean/rvar nullable: track_running_stats off).
@@ -269,17 +312,17 @@ UBPL_API int ubpl_bn_forward_stats(const float* x, int B, int C, int HW, const f
     const int splits = splits_for(B, C);
     const int bper = (B + splits - 1) / splits;
     const int gs = (B + bper - 1) / bper;
+    if (C > MAXBN) return (int)hipErrorInvalidValue;
+    unsigned* cnt = reinterpret_cast<unsigned*>(part);
+    part += CNT_DOUBLES;
+    const StatsOut o{gamma, beta, eps, momentum, rmean, rvar, mean_out, invstd_out, scale, shift};
     const bool vec = (HW % 4 == 0) && (((uintptr_t)x & 15) == 0);
     if (vec)
-        hipLaunchKernelGGL(stats_partial_kernel<true>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, x, B, C, HW,
-                           bper, part);
+        hipLaunchKernelGGL(stats_kernel<true>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, x, B, C, HW, bper, part,
+                           cnt, o);
     else
-        hipLaunchKernelGGL(stats_partial_kernel<false>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, x, B, C, HW,
-                           bper, part);
-    UBPL_LAUNCH_CHECK();
-    hipLaunchKernelGGL(stats_finalize_kernel, dim3(ubpl::cdiv(C, 64)), dim3(64), 0, (hipStream_t)stream, x, part, C,
-                       HW, gs, (int64_t)B * HW, gamma, beta, eps, momentum, rmean, rvar, mean_out, invstd_out, scale,
-                       shift);
+        hipLaunchKernelGGL(stats_kernel<false>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, x, B, C, HW, bper,
+                           part, cnt, o);
     UBPL_LAUNCH_CHECK();
     return 0;
 }
@@ -315,18 +358,19 @@ UBPL_API int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int
     const int gs = (B + bper - 1) / bper;
     const uintptr_t al = (uintptr_t)dz | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)add1 | (uintptr_t)add2;
     const bool vec = (HW % 4 == 0) && ((al & 15) == 0);
-    if (vec)
-        hipLaunchKernelGGL(bwd_partial_kernel<true>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
-                           bper, scale, shift, mean, relu, part);
-    else
-        hipLaunchKernelGGL(bwd_partial_kernel<false>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
-                           bper, scale, shift, mean, relu, part);
-    UBPL_LAUNCH_CHECK();
     float* ca = coef;
     float* cb = coef + C;
     float* cc = coef + 2 * C;
-    hipLaunchKernelGGL(bwd_finalize_kernel, dim3(ubpl::cdiv(C, 64)), dim3(64), 0, (hipStream_t)stream, part, C, gs,
-                       (int64_t)B * HW, gamma, invstd, dgamma, dbeta, ca, cb, cc);
+    if (C > MAXBN) return (int)hipErrorInvalidValue;
+    unsigned* cnt = reinterpret_cast<unsigned*>(part);
+    part += CNT_DOUBLES;
+    const BwdOut o{gamma, invstd, dgamma, dbeta, ca, cb, cc};
+    if (vec)
+        hipLaunchKernelGGL(bwd_stats_kernel<true>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
+                           bper, scale, shift, mean, relu, part, cnt, o);
+    else
+        hipLaunchKernelGGL(bwd_stats_kernel<false>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
+                           bper, scale, shift, mean, relu, part, cnt, o);
     UBPL_LAUNCH_CHECK();
     const int64_t total = (int64_t)B * C * HW;
     if (vec)

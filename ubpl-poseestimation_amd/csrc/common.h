@@ -15,6 +15,19 @@ namespace ubpl {
 
 constexpr int WAVE = 64;
 
+// Linear block id L of G -> logical tile id such that consecutive logical ids
+// run on the same XCD (blocks are dispatched round-robin over the 8 XCDs, each
+// with its own L2).  Affinity only: correctness never depends on placement.
+__device__ __forceinline__ int xcd_remap(int L, int G) {
+    constexpr int X = 8;
+    const int q = G / X, r = G % X, x = L % X, s = L / X;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + s;
+}
+
+// Channel group of the conv weight K order: k = (ci/G)*G*T + tap*G + ci%G
+// (G = 16 when it divides the input channels, else all of them).
+__host__ __device__ __forceinline__ int conv_kgroup(int cin) { return (cin % 16 == 0) ? 16 : cin; }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

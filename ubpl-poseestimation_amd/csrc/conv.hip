@@ -6,10 +6,12 @@
 //
 // GEMM view, NCHW, n = b*P + p (P = Ho*Wo, contiguous in memory):
 //   forward  Y[b,m,p] = sum_k W~[m,k] * X~[b,k,p] + bias[m] (+ R[b,m,p])
-//            TAP-MAJOR k = tap*Cin + ci (tap = kh*KS + kw), W~ = the weights
-//            re-laid out [Cout][KS*KS][Cin] (ubpl_conv_weight_tapmajor), so a
-//            K tile of BK channels shares one tap: each thread derives its
-//            input coordinates once per tile, not per element.  X~ = im2col of
+//            GROUPED TAP-MAJOR k = (ci/16)*16T + tap*16 + ci%16 (tap = kh*KS+kw,
+//            T = KS*KS), W~ = the weights re-laid out [Cout][Cin/16][T][16]
+//            (ubpl_conv_weight_tapmajor), so a K tile of BK = 16 channels
+//            shares one tap (input coordinates once per tile, not per element)
+//            and the T taps of one 16-channel group follow each other: the
+//            re-reads of an input row stay inside the L2 working set.  X~ = im2col of
 //            relu(x*scale + shift): the pre-activation BN+ReLU of Residual is
 //            applied while the operand is staged (bn(x) never touches HBM;
 //            scale/shift sit in LDS for the whole workgroup);
@@ -28,6 +30,8 @@
 // 32 consecutive floats per half-wave; register-staged double buffer with one
 // barrier per K step.
 #include "common.h"
+using ubpl::conv_kgroup;
+using ubpl::xcd_remap;
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -37,9 +41,16 @@ constexpr int NT = 256;
 constexpr int BK = 16;
 constexpr int MAXC = 256;  // largest Cin with a fused BN prologue
 
+// component-wise select (a float4 ternary can be lowered to a pointer select through scratch)
+__device__ __forceinline__ float4 sel4(bool ok, float4 v) {
+    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+}
+
+
 // ------------------------------------------------------------------ forward
 // TAPK: k tiles never straddle a tap (Cin % BK == 0 or KS == 1).
-template <int BM, int BN, int KS, int ST, bool PRO, bool VECB, bool TAPK>
+// AVEC: Ktot % 4 == 0 and 16-B aligned weights: float4 weight loads only.
+template <int BM, int BN, int KS, int ST, bool PRO, bool VECB, bool TAPK, bool AVEC>
 __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ bias,
                                                      const float* __restrict__ pscale,
@@ -54,29 +65,32 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
     constexpr int VROWS = NT / (BN / 4);         // vector loader rows per pass
     __shared__ float As[2][BK][ALD];
     __shared__ float Bs[2][BK][BLD];
-    __shared__ float s_sc[PRO ? MAXC : 1], s_sh[PRO ? MAXC : 1];
+    __shared__ float2 s_ss[PRO ? MAXC : 1];   // (scale, shift) per input channel
 
     const int P = Ho * Wo, HWin = H * W;
     const int64_t N = (int64_t)B * P;
     const int Ktot = Cin * KS * KS;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
-    const int m0 = blockIdx.y * BM;
-    const int64_t n0 = (int64_t)blockIdx.x * BN;
-    const int k_begin = blockIdx.z * kchunk;
+    // XCD-aware tile order: the m tiles of one n tile, then neighbouring n
+    // tiles (shared halo rows), share an L2; split-K slowest.
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                              gridDim.x * gridDim.y * gridDim.z);
+    const int by = lam % gridDim.y, bx = (lam / gridDim.y) % gridDim.x, bz = lam / (gridDim.y * gridDim.x);
+    const int m0 = by * BM;
+    const int64_t n0 = (int64_t)bx * BN;
+    const int k_begin = bz * kchunk;
     const int k_end = min(Ktot, k_begin + kchunk);
+    constexpr int T = KS * KS;
+    const int G = conv_kgroup(Cin);
 
     if (PRO) {
-        for (int c = tid; c < Cin; c += NT) {
-            s_sc[c] = pscale[c];
-            s_sh[c] = pshift[c];
-        }
+        for (int c = tid; c < Cin; c += NT) s_ss[c] = make_float2(pscale[c], pshift[c]);
     }
 
     // A loader: row am, k chunk ak0 .. ak0 + A_PER - 1 (vectorised when aligned)
     const int am = tid % BM;
     const int ak0 = (tid / BM) * A_PER;
-    const bool avec = (Ktot % 4) == 0;
     // B loader column(s)
     const int bnl = VECB ? 4 * (tid % (BN / 4)) : tid % BN;
     const int bk0 = VECB ? tid / (BN / 4) : tid / BN;
@@ -93,32 +107,32 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
 
     float ra[A_PER];
     float rb[B_PER];
+    bool b_inb = false;
 
-    // Loads are unconditional at a clamped (always valid) address and masked
-    // afterwards: a load under a per-element branch makes hipcc wait vmcnt(0)
-    // per element (cdna_hip_programming.md §5 'Three .s-level traps' (c)).
+    // Loads are unconditional at a clamped (always valid) address and stay raw
+    // in registers while the K step's MFMAs run; masks and the BN prologue are
+    // applied when the values are stored to LDS.  (A load under a per-element
+    // branch, or a select right after it, makes hipcc wait vmcnt(0) on the spot:
+    // cdna_hip_programming.md §5 'Three .s-level traps' (c).)
     const int am_c = min(m0 + am, Cout - 1);
     const bool am_ok = m0 + am < Cout;
     const float* wrow = w + (int64_t)am_c * Ktot;
     auto load_a = [&](int kt) {
         const int k = kt + ak0;
-        if (avec && k + A_PER <= k_end) {
-            const float4* src = reinterpret_cast<const float4*>(wrow + k);
+        if constexpr (AVEC) {
+            // clamped to the last aligned 4-vector; the tail is masked at store time
+            const float4* src = reinterpret_cast<const float4*>(wrow);
 #pragma unroll
             for (int j = 0; j < A_PER / 4; ++j) {
-                const float4 v = src[j];
-                ra[4 * j] = am_ok ? v.x : 0.f;
-                ra[4 * j + 1] = am_ok ? v.y : 0.f;
-                ra[4 * j + 2] = am_ok ? v.z : 0.f;
-                ra[4 * j + 3] = am_ok ? v.w : 0.f;
+                const float4 v = src[min(k + 4 * j, Ktot - 4) >> 2];
+                ra[4 * j] = v.x;
+                ra[4 * j + 1] = v.y;
+                ra[4 * j + 2] = v.z;
+                ra[4 * j + 3] = v.w;
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < A_PER; ++j) {
-                const int kk = k + j;
-                const float v = wrow[min(kk, Ktot - 1)];
-                ra[j] = (am_ok && kk < k_end) ? v : 0.f;
-            }
+            for (int j = 0; j < A_PER; ++j) ra[j] = wrow[min(k + j, Ktot - 1)];
         }
     };
     auto load_b = [&](int kt) {
@@ -127,38 +141,23 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
             const int p = coh * Wo + cow;
 #pragma unroll
             for (int j = 0; j < BK / VROWS; ++j) {
-                const int k = kt + bk0 + j * VROWS;
-                const bool ok = cvalid && k < k_end;
-                const int kc = min(k, Cin - 1);
-                float4 v = *reinterpret_cast<const float4*>(xb + (int64_t)kc * P + p);
-                if (PRO) {
-                    const float sc = s_sc[kc], sh = s_sh[kc];
-                    v.x = fmaxf(fmaf(v.x, sc, sh), 0.f);
-                    v.y = fmaxf(fmaf(v.y, sc, sh), 0.f);
-                    v.z = fmaxf(fmaf(v.z, sc, sh), 0.f);
-                    v.w = fmaxf(fmaf(v.w, sc, sh), 0.f);
-                }
-                rb[4 * j] = ok ? v.x : 0.f;
-                rb[4 * j + 1] = ok ? v.y : 0.f;
-                rb[4 * j + 2] = ok ? v.z : 0.f;
-                rb[4 * j + 3] = ok ? v.w : 0.f;
+                const int kc = min(kt + bk0 + j * VROWS, Cin - 1);
+                const float4 v = *reinterpret_cast<const float4*>(xb + (int64_t)kc * P + p);
+                rb[4 * j] = v.x;
+                rb[4 * j + 1] = v.y;
+                rb[4 * j + 2] = v.z;
+                rb[4 * j + 3] = v.w;
             }
         } else if constexpr (TAPK) {
-            // one tap for the whole K tile: input coordinates once per tile
-            const int tap = kt / Cin, ci0 = kt - tap * Cin;
+            // one (channel group, tap) per K tile (G == BK): input coordinates once per tile
+            const int kg = kt / BK;
+            const int tap = kg % T, ci0 = (kg / T) * BK;
             const int kh = tap / KS, kw = tap - kh * KS;
             const int ih = coh * ST - PADK + kh, iw = cow * ST - PADK + kw;
-            const bool inb = cvalid && ih >= 0 && ih < H && iw >= 0 && iw < W;
-            const float* src = xb + (inb ? ih * W + iw : 0);
+            b_inb = cvalid && ih >= 0 && ih < H && iw >= 0 && iw < W;
+            const float* src = xb + (b_inb ? ih * W + iw : 0);
 #pragma unroll
-            for (int j = 0; j < B_PER; ++j) {
-                const int r = bk0 + j * (NT / BN);
-                const bool ok = inb && kt + r < k_end;
-                const int ci = min(ci0 + r, Cin - 1);
-                float v = src[(int64_t)ci * HWin];
-                if (PRO) v = fmaxf(fmaf(v, s_sc[ci], s_sh[ci]), 0.f);
-                rb[j] = ok ? v : 0.f;
-            }
+            for (int j = 0; j < B_PER; ++j) rb[j] = src[(int64_t)min(ci0 + bk0 + j * (NT / BN), Cin - 1) * HWin];
         } else {
             // generic (stem, Cin = 3): tap and channel per element
 #pragma unroll
@@ -166,26 +165,55 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
                 const int k = kt + bk0 + j * (NT / BN);
                 float v = 0.f;
                 if (cvalid && k < k_end) {
-                    const int tap = k / Cin, ci = k - tap * Cin;
+                    const int cb = k / (G * T), rem = k - cb * G * T;
+                    const int tap = rem / G, ci = cb * G + (rem - (rem / G) * G);
                     const int kh = tap / KS, kw = tap - kh * KS;
                     const int ih = coh * ST - PADK + kh, iw = cow * ST - PADK + kw;
                     if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
                         v = xb[(int64_t)ci * HWin + ih * W + iw];
-                        if (PRO) v = fmaxf(fmaf(v, s_sc[ci], s_sh[ci]), 0.f);
+                        if (PRO) v = fmaxf(fmaf(v, s_ss[ci].x, s_ss[ci].y), 0.f);
                     }
                 }
                 rb[j] = v;
             }
         }
     };
-    auto store_ab = [&](int buf) {
+    // prologue evaluated unconditionally, then selected (a conditional LDS read
+    // becomes an exec-mask branch with its own lgkmcnt wait)
+    auto store_ab = [&](int buf, int kt) {
+        {
+            const int k = kt + ak0;
 #pragma unroll
-        for (int j = 0; j < A_PER; ++j) As[buf][ak0 + j][am] = ra[j];
+            for (int j = 0; j < A_PER; ++j) As[buf][ak0 + j][am] = (am_ok && k + j < k_end) ? ra[j] : 0.f;
+        }
         if constexpr (VECB) {
 #pragma unroll
-            for (int j = 0; j < BK / VROWS; ++j)
-                *reinterpret_cast<float4*>(&Bs[buf][bk0 + j * VROWS][bnl]) =
-                    make_float4(rb[4 * j], rb[4 * j + 1], rb[4 * j + 2], rb[4 * j + 3]);
+            for (int j = 0; j < BK / VROWS; ++j) {
+                const int k = kt + bk0 + j * VROWS;
+                const bool ok = cvalid && k < k_end;
+                float4 v = make_float4(rb[4 * j], rb[4 * j + 1], rb[4 * j + 2], rb[4 * j + 3]);
+                if (PRO) {
+                    const float2 ss = s_ss[min(k, Cin - 1)];
+                    v.x = fmaxf(fmaf(v.x, ss.x, ss.y), 0.f);
+                    v.y = fmaxf(fmaf(v.y, ss.x, ss.y), 0.f);
+                    v.z = fmaxf(fmaf(v.z, ss.x, ss.y), 0.f);
+                    v.w = fmaxf(fmaf(v.w, ss.x, ss.y), 0.f);
+                }
+                *reinterpret_cast<float4*>(&Bs[buf][bk0 + j * VROWS][bnl]) = sel4(ok, v);
+            }
+        } else if constexpr (TAPK) {
+            const int ci0 = ((kt / BK) / T) * BK;
+#pragma unroll
+            for (int j = 0; j < B_PER; ++j) {
+                const int r = bk0 + j * (NT / BN);
+                const bool ok = b_inb && kt + r < k_end;
+                float v = rb[j];
+                if (PRO) {
+                    const float2 ss = s_ss[min(ci0 + r, Cin - 1)];
+                    v = fmaxf(fmaf(v, ss.x, ss.y), 0.f);
+                }
+                Bs[buf][r][bnl] = ok ? v : 0.f;
+            }
         } else {
 #pragma unroll
             for (int j = 0; j < B_PER; ++j) Bs[buf][bk0 + j * (NT / BN)][bnl] = rb[j];
@@ -205,15 +233,16 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
     if (nkt > 0) {
         load_a(k_begin);
         load_b(k_begin);
-        store_ab(0);
+        store_ab(0, k_begin);
     }
     __syncthreads();
     const int li = lane & 31, lk = lane >> 5;
     for (int t = 0; t < nkt; ++t) {
         const int cur = t & 1;
+        const int knext = k_begin + (t + 1) * BK;
         if (t + 1 < nkt) {
-            load_a(k_begin + (t + 1) * BK);
-            load_b(k_begin + (t + 1) * BK);
+            load_a(knext);
+            load_b(knext);
         }
 #pragma unroll
         for (int s = 0; s < BK / 2; ++s) {
@@ -229,14 +258,14 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
         }
         if (t + 1 < nkt) {
-            store_ab(cur ^ 1);
+            store_ab(cur ^ 1, knext);
             __syncthreads();
         }
     }
 
     if (slab != nullptr) {
         // split-K partial tile: slab[z][m][n]
-        float* sl = slab + (int64_t)blockIdx.z * Cout * N;
+        float* sl = slab + (int64_t)bz * Cout * N;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int64_t n = n0 + wn + 32 * j + li;
@@ -251,27 +280,41 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
         }
         return;
     }
-    // ---- epilogue: + bias (+ residual), coalesced along n
+    // ---- epilogue: + bias (+ residual), coalesced along n.  Two phases: res
+    // may alias y, so every residual load is issued before the first store
+    // (interleaved, each load would wait for the previous store).  An element
+    // is read and written by the same thread, so aliasing stays correct.
+    int64_t obase[TN];
+    bool nok[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int64_t n = n0 + wn + 32 * j + li;
-        if (n >= N) continue;
-        const int b = (int)(n / P);
-        const int p = (int)(n - (int64_t)b * P);
+        nok[j] = n < N;
+        const int64_t nc = nok[j] ? n : N - 1;
+        const int b = (int)(nc / P);
+        const int p = (int)(nc - (int64_t)b * P);
+        obase[j] = (int64_t)b * Cout * P + p;
+    }
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk, Cout - 1);
+                if (bias) acc[i][j][r] += bias[m];
+                if (res) acc[i][j][r] += res[obase[j] + (int64_t)m * P];
+            }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        if (!nok[j]) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-                if (m < Cout) {
-                    const int64_t o = ((int64_t)b * Cout + m) * P + p;
-                    float v = acc[i][j][r];
-                    if (bias) v += bias[m];
-                    if (res) v += res[o];
-                    y[o] = v;
-                }
+                if (m < Cout) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
             }
-        }
     }
 }
 
@@ -450,11 +493,6 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
     if (bias_blk && tid < BM && m0 + tid < Cout) sl[(int64_t)(m0 + tid) * Nt + Ntot] = bsum;
 }
 
-// component-wise select (a float4 ternary can be lowered to a pointer select through scratch)
-__device__ __forceinline__ float4 sel4(bool ok, float4 v) {
-    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
-}
-
 // ------------------------------------------------------------------ wgrad v2
 // Both operands run along k = b*P + p in memory (dY[b][m][p], x[b][ci][p']),
 // so they are staged k-contiguous: float4 global loads, As[m][16] / Bs[n][16]
@@ -483,11 +521,16 @@ __global__ void __launch_bounds__(NT, 4) conv_wgrad2_kernel(const float* __restr
     const int Ntot = Cin * KS * KS, Nt = Ntot + 1;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
-    const int m0 = blockIdx.y * BM, nb0 = blockIdx.x * BN;
-    const int k_begin = blockIdx.z * kchunk;
+    // XCD-aware tile order: the n tiles (taps) and m tiles of one k split read
+    // the same dy / x rows and share an L2.
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                              gridDim.x * gridDim.y * gridDim.z);
+    const int bx = lam % gridDim.x, by = (lam / gridDim.x) % gridDim.y, bz = lam / (gridDim.x * gridDim.y);
+    const int m0 = by * BM, nb0 = bx * BN;
+    const int k_begin = bz * kchunk;
     const int k_end = min(Kall, k_begin + kchunk);
     const int q = tid & 3, r0 = tid >> 2;
-    const bool bias_blk = with_bias && blockIdx.x == 0;
+    const bool bias_blk = with_bias && bx == 0;
 
     if (PRO) {
         for (int c = tid; c < Cin; c += NT) {
@@ -626,7 +669,7 @@ __global__ void __launch_bounds__(NT, 4) conv_wgrad2_kernel(const float* __restr
         }
     }
 
-    float* sl = slab + (int64_t)blockIdx.z * Cout * Nt;
+    float* sl = slab + (int64_t)bz * Cout * Nt;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int n = nb0 + wn + 32 * j + li;
@@ -718,55 +761,54 @@ int launch_wgrad_reduce(const float* slab, int splits, int Cout, int Cin, int T,
     return 0;
 }
 
-// wt[co][tap][ci] = w[co][ci][tap]
-__global__ void tapmajor_kernel(const float* __restrict__ w, int Cout, int Cin, int T, float* __restrict__ wt) {
-    const int64_t total = (int64_t)Cout * Cin * T;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int ci = (int)(i % Cin);
-        const int64_t t = i / Cin;
-        const int tap = (int)(t % T);
-        const int co = (int)(t / T);
-        wt[i] = w[((int64_t)co * Cin + ci) * T + tap];
-    }
+// Forward weight layout (grouped tap-major): wt[co][ci/G][tap][ci%G] = w[co][ci][tap].
+__device__ __forceinline__ int64_t fwd_layout_src(int64_t i, int Cout, int Cin, int T) {
+    const int G = conv_kgroup(Cin);
+    const int gi = (int)(i % G);
+    const int64_t t1 = i / G;
+    const int tap = (int)(t1 % T);
+    const int64_t t2 = t1 / T;
+    const int cb = (int)(t2 % (Cin / G));
+    const int co = (int)(t2 / (Cin / G));
+    return ((int64_t)co * Cin + cb * G + gi) * T + tap;
 }
 
-// dgrad weights, tap-major: wd[ci][tap][co] = w[co][ci][T-1-tap]
+// dgrad weights = the forward layout of the flipped, transposed kernel:
+// wd[ci][co/G][tap][co%G] = w[co][ci][T-1-tap]  (G = conv_kgroup(Cout)).
+__device__ __forceinline__ int64_t dgrad_layout_src(int64_t i, int Cout, int Cin, int T) {
+    const int G = conv_kgroup(Cout);
+    const int gi = (int)(i % G);
+    const int64_t t1 = i / G;
+    const int tap = (int)(t1 % T);
+    const int64_t t2 = t1 / T;
+    const int cb = (int)(t2 % (Cout / G));
+    const int ci = (int)(t2 / (Cout / G));
+    return ((int64_t)(cb * G + gi) * Cin + ci) * T + (T - 1 - tap);
+}
+
+__global__ void tapmajor_kernel(const float* __restrict__ w, int Cout, int Cin, int T, float* __restrict__ wt) {
+    const int64_t total = (int64_t)Cout * Cin * T;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+        wt[i] = w[fwd_layout_src(i, Cout, Cin, T)];
+}
+
 __global__ void flip_tapmajor_kernel(const float* __restrict__ w, int Cout, int Cin, int T, float* __restrict__ wd) {
     const int64_t total = (int64_t)Cout * Cin * T;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int co = (int)(i % Cout);
-        const int64_t t = i / Cout;
-        const int tap = (int)(t % T);
-        const int ci = (int)(t / T);
-        wd[i] = w[((int64_t)co * Cin + ci) * T + (T - 1 - tap)];
-    }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+        wd[i] = w[dgrad_layout_src(i, Cout, Cin, T)];
 }
 
 // Batched weight re-layout over a segment table (int64 [nseg][5]:
 // src_off, dst_off, Cout, Cin, T), one segment per blockIdx.y.
-// mode 0: tap-major forward layout  dst[co][tap][ci] = src[co][ci][tap]
-// mode 1: dgrad layout               dst[ci][tap][co] = src[co][ci][T-1-tap]
+// mode 0: forward layout, mode 1: dgrad layout (above).
 __global__ void __launch_bounds__(256) relayout_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                       const int64_t* __restrict__ table, int mode) {
     const int64_t* e = table + (int64_t)blockIdx.y * 5;
     const int64_t so = e[0], dof = e[1];
     const int Cout = (int)e[2], Cin = (int)e[3], T = (int)e[4];
     const int64_t total = (int64_t)Cout * Cin * T;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        if (mode == 0) {
-            const int ci = (int)(i % Cin);
-            const int64_t t = i / Cin;
-            const int tap = (int)(t % T);
-            const int co = (int)(t / T);
-            dst[dof + i] = src[so + ((int64_t)co * Cin + ci) * T + tap];
-        } else {
-            const int co = (int)(i % Cout);
-            const int64_t t = i / Cout;
-            const int tap = (int)(t % T);
-            const int ci = (int)(t / T);
-            dst[dof + i] = src[so + ((int64_t)co * Cin + ci) * T + (T - 1 - tap)];
-        }
-    }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+        dst[dof + i] = src[so + (mode == 0 ? fwd_layout_src(i, Cout, Cin, T) : dgrad_layout_src(i, Cout, Cin, T))];
 }
 
 struct Plan {
@@ -839,14 +881,14 @@ Plan fwd_plan(int Cout, int64_t N, int Ktot, int bn) {
     return best;
 }
 
-template <int BM, int BN, int KS, int ST, bool PRO, bool VECB, bool TAPK>
+template <int BM, int BN, int KS, int ST, bool PRO, bool VECB, bool TAPK, bool AVEC>
 int launch_fwd(const float* x, const float* w, const float* bias, const float* ps, const float* sh, const float* res,
                float* y, int B, int Cin, int H, int W, int Cout, int Ho, int Wo, const Plan& pl, float* slab,
                hipStream_t st) {
     const int64_t N = (int64_t)B * Ho * Wo;
     dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
     const bool split = pl.splits > 1;
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, KS, ST, PRO, VECB, TAPK>), grid, dim3(NT), 0, st, x, w, bias, ps, sh,
+    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, KS, ST, PRO, VECB, TAPK, AVEC>), grid, dim3(NT), 0, st, x, w, bias, ps, sh,
                        split ? nullptr : res, y, B, Cin, H, W, Cout, Ho, Wo, pl.kchunk, split ? slab : nullptr);
     UBPL_LAUNCH_CHECK();
     if (split) {
@@ -860,15 +902,32 @@ int launch_fwd(const float* x, const float* w, const float* bias, const float* p
     return 0;
 }
 
+template <int KS, int ST, bool PRO, bool VECB, bool TAPK, bool AVEC>
+int fwd_bm2(const Plan& pl, const float* x, const float* w, const float* bias, const float* ps, const float* sh,
+            const float* res, float* y, int B, int Cin, int H, int W, int Cout, int Ho, int Wo, float* slab,
+            hipStream_t st) {
+    if (pl.bm == 128)
+        return launch_fwd<128, 128, KS, ST, PRO, VECB, TAPK, AVEC>(x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout,
+                                                                  Ho, Wo, pl, slab, st);
+    return launch_fwd<64, 128, KS, ST, PRO, VECB, TAPK, AVEC>(x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo,
+                                                             pl, slab, st);
+}
+
+// AVEC (float4 weight rows) when Ktot % 4 == 0 and w is 16-B aligned; KS = 3
+// (Cin % 16 == 0) always qualifies, the stem (Cin = 3) never does.
 template <int KS, int ST, bool PRO, bool VECB, bool TAPK>
 int fwd_bm(const Plan& pl, const float* x, const float* w, const float* bias, const float* ps, const float* sh,
            const float* res, float* y, int B, int Cin, int H, int W, int Cout, int Ho, int Wo, float* slab,
            hipStream_t st) {
-    if (pl.bm == 128)
-        return launch_fwd<128, 128, KS, ST, PRO, VECB, TAPK>(x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo,
-                                                            pl, slab, st);
-    return launch_fwd<64, 128, KS, ST, PRO, VECB, TAPK>(x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo, pl,
-                                                       slab, st);
+    const bool avec = ((Cin * KS * KS) % 4 == 0) && (((uintptr_t)w & 15) == 0);
+    if constexpr (KS == 7) {
+        return fwd_bm2<KS, ST, PRO, VECB, TAPK, false>(pl, x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st);
+    } else {
+        if (avec)
+            return fwd_bm2<KS, ST, PRO, VECB, TAPK, true>(pl, x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st);
+        if constexpr (KS == 3) return (int)hipErrorInvalidValue;
+        else return fwd_bm2<KS, ST, PRO, VECB, TAPK, false>(pl, x, w, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo, slab, st);
+    }
 }
 
 template <int BM, int BN, int KS, int ST, bool PRO, bool VEC1>
@@ -967,10 +1026,10 @@ const Device& device_info() {
             hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
             r.ncu = v;
         int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_fwd_kernel<128, 128, 3, 1, true, false, true>, NT,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_fwd_kernel<128, 128, 3, 1, true, false, true, true>, NT,
                                                          0) == hipSuccess && o > 0)
             r.occ_fwd128 = o;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_fwd_kernel<64, 128, 3, 1, true, false, true>, NT,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_fwd_kernel<64, 128, 3, 1, true, false, true, true>, NT,
                                                          0) == hipSuccess && o > 0)
             r.occ_fwd64 = o;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, conv_wgrad_kernel<64, 64, 3, 1, true, true>, NT, 0) ==
@@ -1093,7 +1152,8 @@ UBPL_API int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, 
     return launch_wgrad_reduce(slab, splits, Cout, Cin, KS * KS, wb, dw, db, accumulate, st);
 }
 
-// Forward weight layout for KS > 1: wt[co][tap][ci] = w[co][ci][tap].
+// Forward weight layout: wt[co][ci/G][tap][ci%G] = w[co][ci][tap], G = 16 if it
+// divides Cin, else Cin (plain tap-major); for KS == 1 it is w itself.
 UBPL_API int ubpl_conv_weight_tapmajor(const float* w, int Cout, int Cin, int KS, float* wt, void* stream) {
     const int64_t total = (int64_t)Cout * Cin * KS * KS;
     int grid = (int)((total + 255) / 256);
@@ -1103,8 +1163,8 @@ UBPL_API int ubpl_conv_weight_tapmajor(const float* w, int Cout, int Cin, int KS
     return 0;
 }
 
-// dgrad weights (stride 1): wd[ci][tap][co] = w[co][ci][KS*KS-1-tap], i.e. the
-// tap-major forward layout of the flipped, transposed kernel: dx = conv(dy, wd).
+// dgrad weights (stride 1): the forward layout of the flipped, transposed
+// kernel, wd[ci][co/G][tap][co%G] = w[co][ci][KS*KS-1-tap]: dx = conv(dy, wd).
 UBPL_API int ubpl_conv_weight_flip(const float* w, int Cout, int Cin, int KS, float* wt, void* stream) {
     const int64_t total = (int64_t)Cout * Cin * KS * KS;
     int grid = (int)((total + 255) / 256);

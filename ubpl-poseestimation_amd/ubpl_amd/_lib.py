@@ -28,6 +28,7 @@ SIGNATURES = {
     "ubpl_adamw_step": (I, [P, P, P, P, L, D, D, D, D, D, L, P]),
     "ubpl_scale_": (I, [P, L, F, P]),
     "ubpl_bn_splits": (I, [I, I]),
+    "ubpl_bn_part_doubles": (L, [I, I]),
     "ubpl_bn_forward_stats": (I, [P, I, I, I, P, P, F, F, P, P, P, P, P, P, P, P]),
     "ubpl_bn_eval_coeffs": (I, [P, P, P, P, F, I, P, P, P]),
     "ubpl_bn_apply": (I, [P, I, I, I, P, P, I, P, P]),

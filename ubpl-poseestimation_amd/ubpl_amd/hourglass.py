@@ -281,8 +281,9 @@ class StackedHourglass(nn.Module):
         if key not in self._ws:
             n = 0
             for c in (64, 128, 256, 512):
-                n = max(n, 2 * c * Kn.bn_splits(B, c))
-            self._ws[key] = torch.empty(n, dtype=torch.float64, device=self.flat_params.device)
+                n = max(n, int(_lib.lib().ubpl_bn_part_doubles(B, c)))
+            # zeroed once: the arrival counters at its tail reset themselves
+            self._ws[key] = torch.zeros(n, dtype=torch.float64, device=self.flat_params.device)
             self._ws[("coef", B)] = torch.empty(3 * 512, device=self.flat_params.device)
         return self._ws[key]
 

@@ -195,6 +195,11 @@ def bn_splits(B, C):
     return _lib.lib().ubpl_bn_splits(B, C)
 
 
+def bn_part(B, C, device):
+    """Zeroed BN scratch (partial sums + self-resetting arrival counters)."""
+    return torch.zeros(int(_lib.lib().ubpl_bn_part_doubles(B, C)), dtype=torch.float64, device=device)
+
+
 def bn_forward_stats(x, gamma, beta, eps, momentum, rmean, rvar, part, mean, invstd, scale, shift):
     B, C = x.shape[:2]
     HW = x[0, 0].numel()
@@ -239,8 +244,9 @@ def conv_weight_tapmajor(w):
 
 
 def conv2d_forward(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out=None, w_tap=None):
-    """w: reference layout [Cout,Cin,KS,KS] (re-laid out tap-major here for
-    KS > 1) — or pass w_tap, an already tap-major [Cout,KS*KS,Cin] copy."""
+    """w: reference layout [Cout,Cin,KS,KS] (re-laid out here for KS > 1) — or
+    pass w_tap, an already re-laid-out copy viewed as [Cout,KS*KS,Cin] (its
+    element order is ubpl_conv_weight_tapmajor's grouped tap-major layout)."""
     B, Cin, H, W = x.shape
     if w_tap is not None:
         Cout, T, wc = w_tap.shape
@@ -270,7 +276,7 @@ def conv2d_wgrad(dy, x, KS, stride, dw, db, pscale=None, pshift=None, accumulate
 
 
 def conv_weight_flip(w):
-    """Tap-major [Cin, KS*KS, Cout] weights of the data gradient (stride 1)."""
+    """Data-gradient weights (stride 1), viewed as [Cin, KS*KS, Cout]."""
     Cout, Cin, KS, _ = w.shape
     wt = torch.empty((Cin, KS * KS, Cout), device=w.device, dtype=F32)
     call("ubpl_conv_weight_flip", _p(w), Cout, Cin, KS, _p(wt), stream())

@@ -22,6 +22,9 @@ and keep their own BN statistics; EMA alpha is keyed on the epoch; the FDL
 term is added to both students' totals (its gradient applied twice); the
 pseudo-loss normaliser counts rows with a positive weighted loss.
 """
+import contextlib
+import os
+
 import torch
 
 from . import dist as D
@@ -136,6 +139,42 @@ def _sync_stats(local_sums, counts):
 # ---------------------------------------------------------------------------
 # MT_UBPL
 # ---------------------------------------------------------------------------
+class _ModelStreams:
+    """One HIP stream per student (its teacher's forward rides along).  The
+    networks are independent until the losses, and their small hourglass
+    levels (<= 16x16: a few dozen workgroups per launch) leave most of the
+    chip idle, so two networks in flight fill it.  Autograd runs each
+    network's backward on its forward's stream (PyTorch stream semantics of
+    backward), so the backward overlaps the same way.  UBPL_MODEL_STREAMS=0
+    runs everything on the current stream."""
+    _cache = {}
+
+    def __init__(self, M, dev):
+        self.main = torch.cuda.current_stream(dev)
+        key = (M, dev.index)
+        if key not in self._cache:
+            self._cache[key] = [torch.cuda.Stream(device=dev) for _ in range(M)]
+        self.side = self._cache[key]
+        for s in self.side:
+            s.wait_stream(self.main)
+
+    @staticmethod
+    def make(M, dev):
+        if M < 2 or os.environ.get("UBPL_MODEL_STREAMS", "1") == "0":
+            return None
+        return _ModelStreams(M, dev)
+
+    def on(self, mi):
+        return torch.cuda.stream(self.side[mi])
+
+    def join(self, tensors=()):
+        for s in self.side:
+            self.main.wait_stream(s)
+        for t in tensors:                 # produced on a side stream, used on main
+            if t is not None and t.is_cuda:
+                t.record_stream(self.main)
+
+
 def _backward_all(totals):
     """The reference runs total_i.backward(retain_graph=True) once per student
     (projects/MT_UBPL.py:334-336): the shared FDL term makes every call reach
@@ -170,17 +209,21 @@ def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
         nega = _w(isl, 0.0, args.pseudoWeight)                   # getSampleWeight_nega
         B = imgs[0].shape[0]
         outs, feats, outs_ema = [], [], []
+        mstreams = _ModelStreams.make(M, dev)
         for mi in range(M):                                      # :228-243
             oa, fa, ea = [], [], []
-            for a in range(A):
-                o, f = models[mi](imgs[a])
-                oa.append(o)
-                fa.append(f)
-                with torch.no_grad():
-                    ea.append(models_ema[mi](imgs[a])[0])
+            with (mstreams.on(mi) if mstreams else contextlib.nullcontext()):
+                for a in range(A):
+                    o, f = models[mi](imgs[a])
+                    oa.append(o)
+                    fa.append(f)
+                    with torch.no_grad():
+                        ea.append(models_ema[mi](imgs[a])[0])
             outs.append(oa)
             feats.append(fa)
             outs_ema.append(ea)
+        if mstreams:
+            mstreams.join([t for grp in (outs, feats, outs_ema) for ts in grp for t in ts])
         K = outs[0][0].shape[2]
         # ---- loss sums / counts on device
         sums, cnts = [], []
@@ -225,6 +268,8 @@ def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
             totals.append(pec + mtc + epc + fdc)
             rec.append((pec, mtc, epc))
         _backward_all(totals)                                     # :334-336
+        if mstreams:
+            mstreams.join()
         D.allreduce_grads(models)
         for o in optims:
             o.step()
