@@ -140,10 +140,10 @@ def _sync_stats(local_sums, counts):
 # MT_UBPL
 # ---------------------------------------------------------------------------
 class _ModelStreams:
-    """One HIP stream per student (its teacher's forward rides along).  The
+    """One HIP stream per network (students 0..M-1, then their teachers).  The
     networks are independent until the losses, and their small hourglass
     levels (<= 16x16: a few dozen workgroups per launch) leave most of the
-    chip idle, so two networks in flight fill it.  Autograd runs each
+    chip idle, so several networks in flight fill it.  Autograd runs each
     network's backward on its forward's stream (PyTorch stream semantics of
     backward), so the backward overlaps the same way.  UBPL_MODEL_STREAMS=0
     runs everything on the current stream."""
@@ -153,8 +153,9 @@ class _ModelStreams:
         self.main = torch.cuda.current_stream(dev)
         key = (M, dev.index)
         if key not in self._cache:
-            self._cache[key] = [torch.cuda.Stream(device=dev) for _ in range(M)]
+            self._cache[key] = [torch.cuda.Stream(device=dev) for _ in range(2 * M)]
         self.side = self._cache[key]
+        self.M = M
         for s in self.side:
             s.wait_stream(self.main)
 
@@ -166,6 +167,9 @@ class _ModelStreams:
 
     def on(self, mi):
         return torch.cuda.stream(self.side[mi])
+
+    def on_teacher(self, mi):
+        return torch.cuda.stream(self.side[self.M + mi])
 
     def join(self, tensors=()):
         for s in self.side:
@@ -217,6 +221,8 @@ def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
                     o, f = models[mi](imgs[a])
                     oa.append(o)
                     fa.append(f)
+            with (mstreams.on_teacher(mi) if mstreams else contextlib.nullcontext()):
+                for a in range(A):
                     with torch.no_grad():
                         ea.append(models_ema[mi](imgs[a])[0])
             outs.append(oa)
