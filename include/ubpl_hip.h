@@ -79,6 +79,10 @@ int ubpl_ema_update(float* ema, const float* p, int64_t n, double alpha, void* s
 /* torch.optim.AdamW step (the optimizer projects/MT_UBPL.py:48 builds) on flat buffers. */
 int ubpl_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
                     double eps, double weight_decay, int64_t step, void* stream);
+/* The same step with the 1-based step count on the device (incremented by the
+ * call), so a captured HIP graph of the training step replays it; coef: 4 floats. */
+int ubpl_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
+                        double beta2, double eps, double weight_decay, int64_t* step, float* coef, void* stream);
 int ubpl_scale_(float* x, int64_t n, float s, void* stream);
 
 /* ---------------------------------------------------------------- H2-H4 --

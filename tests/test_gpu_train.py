@@ -123,3 +123,35 @@ def test_train_step_vs_reference(case, flat_adam):
             else:
                 err = float((b.cpu().double() - rb.double()).norm() / (rb.double().norm() + 1e-30))
                 assert err < 1e-3, (mi, bn, err)
+
+
+def test_step_graph_replay_matches_eager(monkeypatch):
+    """Four MT_UBPL steps with the step graph (2 eager warm-up steps, capture,
+    2 replays) leave the students, teachers and BN statistics bit-identical to
+    four eager steps: the replay runs the same kernels in the same per-stream
+    order, with the AdamW step count and the BN arrival counters on the device."""
+    from ubpl_amd import train as T
+    from ubpl_amd.optim import FlatAdamW
+    cfg = seeds.step_cases()["mt_ubpl"]
+
+    def run(graph):
+        monkeypatch.setenv("UBPL_STEP_GRAPH", "1" if graph else "0")
+        models, emas, _ = seeds.step_models(_factory, cfg, device="cuda")
+        optims = [FlatAdamW(m, lr=cfg["lr"], weight_decay=0) for m in models]
+        loader, args = seeds.step_batch(cfg, OR.kps_heatmap_torch)
+        import io
+        import contextlib
+        with contextlib.redirect_stdout(io.StringIO()):
+            rec = T.train_mt_ubpl(list(loader) * 4, models, emas, optims, args)
+        runner = T._StepGraph.get(T._mt_ubpl_core, models, emas, optims, args)
+        assert (runner.graph is not None) == graph
+        torch.cuda.synchronize()
+        return [m.flat_params.clone() for m in models + emas], [m.flat_stats.clone() for m in models + emas], rec
+
+    p_e, s_e, r_e = run(False)
+    p_g, s_g, r_g = run(True)
+    for a, b in zip(p_e, p_g):
+        assert torch.equal(a, b)
+    for a, b in zip(s_e, s_g):
+        assert torch.equal(a, b)
+    assert _flat(r_e, []) == _flat(r_g, [])

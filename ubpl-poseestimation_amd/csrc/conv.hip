@@ -230,19 +230,29 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
 
     if (PRO) __syncthreads();  // s_sc / s_sh ready
     const int nkt = (k_end - k_begin + BK - 1) / BK;
+    // T14 order (cdna_hip_programming.md §5 'glds vs register staging'): tile
+    // t+1 is written to LDS right AFTER the barrier that ends tile t-1's reads,
+    // and tile t+2's loads are issued at once, so every load has a whole K step
+    // of MFMAs to land in.
     if (nkt > 0) {
         load_a(k_begin);
         load_b(k_begin);
         store_ab(0, k_begin);
     }
-    __syncthreads();
+    if (nkt > 1) {
+        load_a(k_begin + BK);
+        load_b(k_begin + BK);
+    }
     const int li = lane & 31, lk = lane >> 5;
     for (int t = 0; t < nkt; ++t) {
         const int cur = t & 1;
-        const int knext = k_begin + (t + 1) * BK;
+        __syncthreads();   // tile t visible; tile t-1's reads of buffer cur^1 done
         if (t + 1 < nkt) {
-            load_a(knext);
-            load_b(knext);
+            store_ab(cur ^ 1, k_begin + (t + 1) * BK);
+            if (t + 2 < nkt) {
+                load_a(k_begin + (t + 2) * BK);
+                load_b(k_begin + (t + 2) * BK);
+            }
         }
 #pragma unroll
         for (int s = 0; s < BK / 2; ++s) {
@@ -256,10 +266,6 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-        }
-        if (t + 1 < nkt) {
-            store_ab(cur ^ 1, knext);
-            __syncthreads();
         }
     }
 
@@ -561,49 +567,40 @@ __global__ void __launch_bounds__(NT, 4) conv_wgrad2_kernel(const float* __restr
         bdw[j] = kw - PADK;
     }
 
+    // raw loads stay in registers across the MFMAs; masks / prologue at store
     float4 ra[AR], rb[BR];
     float bsum[AR];
+    bool kv_st = false;
+    unsigned bmask = 0;          // generic B path: 4 in-bounds bits per staged row
 #pragma unroll
     for (int j = 0; j < AR; ++j) bsum[j] = 0.f;
     auto load = [&](int kt) {
         const int k = kt + 4 * q;
-        const bool kv = k < k_end;                  // k_end % 4 == 0: all four or none
-        const int kc = kv ? k : k_begin;
+        kv_st = k < k_end;                          // k_end % 4 == 0: all four or none
+        const int kc = kv_st ? k : k_begin;
         const int b = kc / P, p = kc - b * P;
 #pragma unroll
-        for (int j = 0; j < AR; ++j) {
-            const float4 v = *reinterpret_cast<const float4*>(dy + ((int64_t)b * Cout + am[j]) * P + p);
-            ra[j] = sel4(kv && aok[j], v);
-        }
+        for (int j = 0; j < AR; ++j)
+            ra[j] = *reinterpret_cast<const float4*>(dy + ((int64_t)b * Cout + am[j]) * P + p);
         if constexpr (VEC1) {
 #pragma unroll
-            for (int j = 0; j < BR; ++j) {
-                float4 v = *reinterpret_cast<const float4*>(x + ((int64_t)b * Cin + bci[j]) * HWin + p);
-                if (PRO) {
-                    const float sc = s_sc[bci[j]], sh = s_sh[bci[j]];
-                    v.x = fmaxf(fmaf(v.x, sc, sh), 0.f);
-                    v.y = fmaxf(fmaf(v.y, sc, sh), 0.f);
-                    v.z = fmaxf(fmaf(v.z, sc, sh), 0.f);
-                    v.w = fmaxf(fmaf(v.w, sc, sh), 0.f);
-                }
-                rb[j] = sel4(kv && bok[j], v);
-            }
+            for (int j = 0; j < BR; ++j)
+                rb[j] = *reinterpret_cast<const float4*>(x + ((int64_t)b * Cin + bci[j]) * HWin + p);
         } else {
             const int oh = p / Wo, ow = p - oh * Wo;   // Wo % 4 == 0: one output row
+            bmask = 0;
 #pragma unroll
             for (int j = 0; j < BR; ++j) {
                 const int ih = oh * ST + bdh[j];
-                const bool rok = kv && bok[j] && ih >= 0 && ih < H;
+                const bool rok = bok[j] && ih >= 0 && ih < H;
                 const float* src = x + ((int64_t)b * Cin + bci[j]) * HWin + (rok ? ih * W : 0);
-                const float sc = PRO ? s_sc[bci[j]] : 1.f, sh = PRO ? s_sh[bci[j]] : 0.f;
                 float e4[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int iw = (ow + e) * ST + bdw[j];
                     const bool ok = rok && iw >= 0 && iw < W;
-                    float v = src[ok ? iw : 0];
-                    if (PRO) v = fmaxf(fmaf(v, sc, sh), 0.f);
-                    e4[e] = ok ? v : 0.f;
+                    e4[e] = src[ok ? iw : 0];
+                    bmask |= (ok ? 1u : 0u) << (4 * j + e);
                 }
                 rb[j] = make_float4(e4[0], e4[1], e4[2], e4[3]);
             }
@@ -613,13 +610,29 @@ __global__ void __launch_bounds__(NT, 4) conv_wgrad2_kernel(const float* __restr
 #pragma unroll
         for (int j = 0; j < AR; ++j) {
             const int row = r0 + 64 * j;
-            As[buf][row * 4 + (q ^ ((row >> 2) & 3))] = ra[j];
-            if (bias_blk) bsum[j] += (ra[j].x + ra[j].y) + (ra[j].z + ra[j].w);
+            const float4 v = sel4(kv_st && aok[j], ra[j]);
+            As[buf][row * 4 + (q ^ ((row >> 2) & 3))] = v;
+            if (bias_blk) bsum[j] += (v.x + v.y) + (v.z + v.w);
         }
 #pragma unroll
         for (int j = 0; j < BR; ++j) {
             const int row = r0 + 64 * j;
-            Bs[buf][row * 4 + (q ^ ((row >> 2) & 3))] = rb[j];
+            float4 v = rb[j];
+            if (PRO) {
+                const float sc = s_sc[bci[j]], sh = s_sh[bci[j]];
+                v.x = fmaxf(fmaf(v.x, sc, sh), 0.f);
+                v.y = fmaxf(fmaf(v.y, sc, sh), 0.f);
+                v.z = fmaxf(fmaf(v.z, sc, sh), 0.f);
+                v.w = fmaxf(fmaf(v.w, sc, sh), 0.f);
+            }
+            if constexpr (VEC1) {
+                v = sel4(kv_st && bok[j], v);
+            } else {
+                const unsigned mj = kv_st ? (bmask >> (4 * j)) : 0u;
+                v = make_float4((mj & 1) ? v.x : 0.f, (mj & 2) ? v.y : 0.f, (mj & 4) ? v.z : 0.f,
+                                (mj & 8) ? v.w : 0.f);
+            }
+            Bs[buf][row * 4 + (q ^ ((row >> 2) & 3))] = v;
         }
     };
 
@@ -632,15 +645,20 @@ __global__ void __launch_bounds__(NT, 4) conv_wgrad2_kernel(const float* __restr
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int nkt = (k_end - k_begin + 15) / 16;
+    // T14 order, as in conv_fwd_kernel
     if (nkt > 0) {
         load(k_begin);
         store(0);
     }
-    __syncthreads();
+    if (nkt > 1) load(k_begin + 16);
     const int li = lane & 31, h = lane >> 5;
     for (int t = 0; t < nkt; ++t) {
         const int cur = t & 1;
-        if (t + 1 < nkt) load(k_begin + (t + 1) * 16);
+        __syncthreads();
+        if (t + 1 < nkt) {
+            store(cur ^ 1);
+            if (t + 2 < nkt) load(k_begin + (t + 2) * 16);
+        }
 #pragma unroll
         for (int q2 = 0; q2 < 2; ++q2) {
             const int sl = 2 * h + q2;
@@ -662,10 +680,6 @@ __global__ void __launch_bounds__(NT, 4) conv_wgrad2_kernel(const float* __restr
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
-        }
-        if (t + 1 < nkt) {
-            store(cur ^ 1);
-            __syncthreads();
         }
     }
 

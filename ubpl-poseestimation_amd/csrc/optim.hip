@@ -68,6 +68,45 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
         adamw_one(p[i], g[i], m[i], v[i], decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
 }
 
+// Graph-replayable AdamW: the step count lives on the device.  adamw_prep
+// increments it and derives (decay, sqrt(bc2), -lr/bc1) exactly as the host
+// path does (f64, then f32); adamw_dev_kernel reads them from memory.
+__global__ void adamw_prep_kernel(int64_t* __restrict__ step, double lr, double beta1, double beta2,
+                                  double weight_decay, float* __restrict__ coef) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int64_t s = ++(*step);
+    const double bc1 = 1.0 - pow(beta1, (double)s);
+    const double bc2 = 1.0 - pow(beta2, (double)s);
+    coef[0] = (float)(1.0 - lr * weight_decay);
+    coef[1] = (float)sqrt(bc2);
+    coef[2] = (float)(-(lr / bc1));
+}
+
+__global__ void __launch_bounds__(256) adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                       const float* __restrict__ coef, float omb1, float b2,
+                                                       float omb2, float eps, int64_t n4) {
+    const float decay = coef[0], bc2_sqrt = coef[1], neg_step = coef[2];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    float4* p4 = reinterpret_cast<float4*>(p);
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    float4* m4 = reinterpret_cast<float4*>(m);
+    float4* v4 = reinterpret_cast<float4*>(v);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 pp = p4[i], mm = m4[i], vv = v4[i];
+        const float4 gg = g4[i];
+        adamw_one(pp.x, gg.x, mm.x, vv.x, decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
+        adamw_one(pp.y, gg.y, mm.y, vv.y, decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
+        adamw_one(pp.z, gg.z, mm.z, vv.z, decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
+        adamw_one(pp.w, gg.w, mm.w, vv.w, decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
+        p4[i] = pp;
+        m4[i] = mm;
+        v4[i] = vv;
+    }
+    for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        adamw_one(p[i], g[i], m[i], v[i], decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
+}
+
 __global__ void __launch_bounds__(256) scale_kernel(float* __restrict__ x, int64_t n, float s) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= s;
@@ -109,6 +148,22 @@ UBPL_API int ubpl_adamw_step(float* p, const float* g, float* m, float* v, int64
     hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
                        (float)(1.0 - lr * weight_decay), (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
                        (float)bc2s, (float)eps, (float)(-step_size), vec4_count(n, p, g, m, v));
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// Same step with the 1-based count on the device (incremented here) so a
+// captured HIP graph replays correctly; coef: scratch of 4 floats.
+UBPL_API int ubpl_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
+                                 double beta2, double eps, double weight_decay, int64_t* step, float* coef,
+                                 void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(adamw_prep_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step, lr, beta1, beta2,
+                       weight_decay, coef);
+    UBPL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, coef,
+                       (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
+                       vec4_count(n, p, g, m, v));
     UBPL_LAUNCH_CHECK();
     return 0;
 }

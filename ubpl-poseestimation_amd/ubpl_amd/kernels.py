@@ -185,6 +185,13 @@ def adamw_step_(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step):
          float(eps), float(weight_decay), int(step), stream())
 
 
+
+def adamw_step_dev_(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step_t, coef):
+    """AdamW with the step count in device memory (int64 scalar, incremented);
+    replayable inside a captured HIP graph.  coef: 4-float scratch."""
+    call("ubpl_adamw_step_dev", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
+         float(eps), float(weight_decay), _p(step_t), _p(coef), stream())
+
 def scale_(x, s):
     _chk(x, "x")
     call("ubpl_scale_", _p(x), x.numel(), float(s), stream())

@@ -23,25 +23,32 @@ class FlatAdamW:
         n = model.n_live
         self.exp_avg = torch.zeros(n, device=model.flat_params.device)
         self.exp_avg_sq = torch.zeros(n, device=model.flat_params.device)
-        self.step_count = 0
+        # the step count lives on the device so a captured step graph replays
+        # it (ubpl_adamw_step_dev increments it); host reads sync lazily
+        self._step_t = torch.zeros((), dtype=torch.int64, device=model.flat_params.device)
+        self._coef = torch.zeros(4, device=model.flat_params.device)
         self.param_groups = [{"lr": lr, "betas": betas, "eps": eps, "weight_decay": weight_decay}]
+
+    @property
+    def step_count(self):
+        return int(self._step_t.item())
 
     def zero_grad(self, set_to_none=True):
         self.model.flat_grads.zero_()
         self.model.attach_grad_views()
 
     def step(self):
-        self.step_count += 1
         g = self.param_groups[0]
-        Kn.adamw_step_(self.model.live_params(), self.model.live_grads(), self.exp_avg, self.exp_avg_sq,
-                       g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self.step_count)
+        Kn.adamw_step_dev_(self.model.live_params(), self.model.live_grads(), self.exp_avg, self.exp_avg_sq,
+                           g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self._step_t,
+                           self._coef)
 
     def state_dict(self):
         return {"state": {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq},
                 "param_groups": [dict(self.param_groups[0])]}
 
     def load_state_dict(self, sd):
-        self.step_count = int(sd["state"]["step"])
+        self._step_t.fill_(int(sd["state"]["step"]))
         self.exp_avg.copy_(sd["state"]["exp_avg"])
         self.exp_avg_sq.copy_(sd["state"]["exp_avg_sq"])
         self.param_groups[0].update(sd["param_groups"][0])

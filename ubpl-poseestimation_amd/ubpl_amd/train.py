@@ -174,6 +174,8 @@ class _ModelStreams:
     def join(self, tensors=()):
         for s in self.side:
             self.main.wait_stream(s)
+        if torch.cuda.is_current_stream_capturing():
+            return                        # the graph's own dependencies order them
         for t in tensors:                 # produced on a side stream, used on main
             if t is not None and t.is_cuda:
                 t.record_stream(self.main)
@@ -189,107 +191,250 @@ def _backward_all(totals):
     torch.autograd.backward(totals)
 
 
+# ---------------------------------------------------------------------------
+# HIP-graph capture of a whole training step
+# ---------------------------------------------------------------------------
+def _flatten(obj, leaves):
+    """Tiny pytree flatten of a batch: tensors become leaves; lists, tuples and
+    dicts recurse; anything else is a constant kept in the spec."""
+    if torch.is_tensor(obj):
+        leaves.append(obj)
+        return ("T", len(leaves) - 1, tuple(obj.shape), str(obj.dtype))
+    if isinstance(obj, (list, tuple)):
+        return (type(obj).__name__, tuple(_flatten(v, leaves) for v in obj))
+    if isinstance(obj, dict):
+        return ("dict", tuple((k, _flatten(v, leaves)) for k, v in obj.items()))
+    return ("C", repr(obj), obj)
+
+
+def _spec_key(spec):
+    if spec[0] == "C":
+        return ("C", spec[1])
+    if spec[0] == "T":
+        return spec
+    if spec[0] == "dict":
+        return ("dict", tuple((k, _spec_key(v)) for k, v in spec[1]))
+    return (spec[0], tuple(_spec_key(v) for v in spec[1]))
+
+
+def _unflatten(spec, leaves):
+    kind = spec[0]
+    if kind == "T":
+        return leaves[spec[1]]
+    if kind == "C":
+        return spec[2]
+    if kind == "dict":
+        return {k: _unflatten(v, leaves) for k, v in spec[1]}
+    vals = [_unflatten(v, leaves) for v in spec[1]]
+    return tuple(vals) if kind == "tuple" else vals
+
+
+class _StepGraph:
+    """Runs a device-only step function (a *_core below) and, once the batch
+    shapes repeat, replays it from a captured HIP graph: ~6k kernel launches
+    per MT_UBPL step become one graph launch, so the host no longer paces the
+    GPU.  The first WARM steps run eagerly on a side stream (graph warm-up
+    rule); the next step is captured (capture records, it does not execute)
+    and then replayed for that batch and every later one, its tensors copied
+    into the graph's static inputs first.  Everything the step reads from the
+    host — args, learning rates — is part of the cache key, so a change
+    re-captures; per-step state (AdamW step counts, BN counters) lives on the
+    device.  One rank only (a collective inside the capture is not assumed
+    safe); UBPL_STEP_GRAPH=0 disables."""
+    WARM = 2
+    _cache = {}
+
+    def __init__(self, core, models, models_ema, optims, args):
+        self.core, self.models, self.emas, self.optims, self.args = core, models, models_ema, optims, args
+        self.enabled = (os.environ.get("UBPL_STEP_GRAPH", "1") != "0" and not D.is_dist()
+                        and all(hasattr(o, "_step_t") for o in optims))
+        self.n_eager = 0
+        self.graph = None
+        self.key = None
+        self.static = None
+        self.out = None
+        self.side = None
+
+    _force_eager = False
+
+    @classmethod
+    def eager(cls):
+        """Context: run steps eagerly (e.g. to time individual kernels with host
+        events, which a captured graph cannot record)."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            old = cls._force_eager
+            cls._force_eager = True
+            try:
+                yield
+            finally:
+                cls._force_eager = old
+        return ctx()
+
+    @classmethod
+    def get(cls, core, models, models_ema, optims, args):
+        akey = repr(sorted(vars(args).items())) if hasattr(args, "__dict__") else repr(args)
+        okey = repr([o.param_groups for o in optims])
+        key = (core.__name__, tuple(map(id, models)), tuple(map(id, models_ema)), tuple(map(id, optims)), akey,
+               okey)
+        if key not in cls._cache:
+            cls._cache[key] = cls(core, models, models_ema, optims, args)
+        return cls._cache[key]
+
+    def _eager(self, batch):
+        return self.core(self.models, self.emas, self.optims, self.args, *batch)
+
+    def run(self, batch, dev):
+        if not self.enabled or self._force_eager:
+            return self._eager(batch)
+        leaves = []
+        spec = _flatten(batch, leaves)
+        key = _spec_key(spec)
+        if self.graph is not None and key == self.key:
+            for dst, src in zip(self.static, leaves):
+                dst.copy_(src, non_blocking=True)
+            self.graph.replay()
+            return self.out
+        if self.n_eager < self.WARM or self.graph is not None:
+            # warm-up (or a batch of another shape): eager, on a side stream
+            if self.side is None:
+                self.side = torch.cuda.Stream(device=dev)
+            main = torch.cuda.current_stream(dev)
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                out = self._eager(batch)
+            main.wait_stream(self.side)
+            self.n_eager += 1
+            return out
+        self.static = [l.to(dev).clone() for l in leaves]
+        sbatch = _unflatten(spec, self.static)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.out = self.core(self.models, self.emas, self.optims, self.args, *sbatch)
+        self.graph, self.key = g, key
+        self.graph.replay()
+        return self.out
+
+
+def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, meta):
+    """One MT_UBPL step (projects/MT_UBPL.py:188-336) on the device with no
+    host synchronisation: returns the packed records [3M+1 losses | counts |
+    pseudo scores] as ONE device tensor and the host-side constants needed to
+    unpack them.  Capturable in a HIP graph (see _StepGraph)."""
+    M = len(models)
+    dev = models[0].flat_params.device
+    S = args.nStack
+    for o in optims:
+        o.zero_grad()
+    A = len(augs_imgMap)
+    imgs = [x.to(dev, non_blocking=True).float().contiguous() for x in augs_imgMap]
+    hms, gates = _targets(imgs, augs_heatmaps, meta, A, dev, args)
+    isl = _islabeled(meta["islabeled"][0], dev)
+    sw = _w(isl, 1.0, 0.0)                                   # getSampleWeight
+    nega = _w(isl, 0.0, args.pseudoWeight)                   # getSampleWeight_nega
+    B = imgs[0].shape[0]
+    outs, feats, outs_ema = [], [], []
+    mstreams = _ModelStreams.make(M, dev)
+    for mi in range(M):                                      # :228-243
+        oa, fa, ea = [], [], []
+        with (mstreams.on(mi) if mstreams else contextlib.nullcontext()):
+            for a in range(A):
+                o, f = models[mi](imgs[a])
+                oa.append(o)
+                fa.append(f)
+        with (mstreams.on_teacher(mi) if mstreams else contextlib.nullcontext()):
+            for a in range(A):
+                with torch.no_grad():
+                    ea.append(models_ema[mi](imgs[a])[0])
+        outs.append(oa)
+        feats.append(fa)
+        outs_ema.append(ea)
+    if mstreams:
+        mstreams.join([t for grp in (outs, feats, outs_ema) for ts in grp for t in ts])
+    K = outs[0][0].shape[2]
+    # ---- loss sums / counts on device
+    sums, cnts = [], []
+    ps_scores = []
+    for mi in range(M):
+        ms = []
+        for a in range(A):
+            s_d, _ = _dist_last(outs[mi][a], outs_ema[mi][a])
+            s_p, c_p = _mse(outs[mi][a], hms[a], S, gates[a], sw.reshape(-1, 1))
+            tg = torch.stack([outs_ema[j][a] for j in range(M)])
+            s_e, c_e, sc_e = _pseudo(outs[mi][a], tg, nega, S, args.pseudoScoreThr)
+            ms.append((s_d, s_p, c_p, s_e, c_e))
+            ps_scores.append(sc_e)
+        sums.append(ms)
+    fd = []
+    if args.FDLWeight > 0:
+        for a in range(A):                                   # :301-330 labeled rows
+            rowmask = _fdl_rows(sw, args)
+            v, c = features_cov(feats[0][a], feats[1][a], rowmask)
+            fd.append((v, c))
+    # pack: per model [mtc_sum, pec_sum, epc_sum], counts [pec_n, epc_n, n_sel] ; fdc
+    loc = []
+    cn = []
+    for mi in range(M):
+        loc += [sum(x[0] for x in sums[mi]), sum(x[1] for x in sums[mi]), sum(x[3] for x in sums[mi])]
+        cn += [sum(x[2][0] for x in sums[mi]), sum(x[4][1] for x in sums[mi]), sum(x[4][2] for x in sums[mi])]
+    if fd:
+        loc.append(sum(v for v, _ in fd))
+        cn.append(sum(c[0] for _, c in fd))
+    counts = torch.stack([c.float() for c in cn])
+    gcounts, gsums = _sync_stats(torch.stack([l.float() for l in loc]), counts)
+    W = D.world()
+    mtc_n = A * B * K * W
+    totals, rec = [], []
+    fdc = 0.
+    if fd:
+        fdc = args.FDLWeight * _norm(loc[-1], gcounts[-1])
+    for mi in range(M):
+        mtc = args.consWeight * (loc[3 * mi] / mtc_n)
+        pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[3 * mi])
+        epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[3 * mi + 1])
+        totals.append(pec + mtc + epc + fdc)
+        rec.append((pec, mtc, epc))
+    _backward_all(totals)                                     # :334-336
+    if mstreams:
+        mstreams.join()
+    D.allreduce_grads(models)
+    for o in optims:
+        o.step()
+    for mi, m in enumerate(models):
+        update_ema_variables(m, models_ema[mi], args)
+    # ---- records: one device->host copy
+    g_rec = []
+    for mi in range(M):
+        g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[3 * mi]),
+                  args.consWeight * gsums[3 * mi] / mtc_n,
+                  args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[3 * mi + 1])]
+    g_rec.append(args.FDLWeight * _norm(gsums[-1], gcounts[-1]) if fd else torch.zeros((), device=dev))
+    score = torch.stack(ps_scores).mean(0)
+    packed = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, score])
+    return packed, (bool(fd), mtc_n, B, len(cn))
+
+
 def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
-    """projects/MT_UBPL.py:157-352 -> (pec_records, mtc_records, epc_records, fdc_record)."""
+    """projects/MT_UBPL.py:157-352 -> (pec_records, mtc_records, epc_records, fdc_record).
+    Steps after the first two are replayed from a captured HIP graph when the
+    batch shapes repeat (UBPL_STEP_GRAPH=0: every step eager)."""
     M = len(models)
     pec_c = [AvgCounter() for _ in range(M)]
     mtc_c = [AvgCounter() for _ in range(M)]
     epc_c = [AvgCounter() for _ in range(M)]
     fdc_c = AvgCounter()
     dev = models[0].flat_params.device
-    S = args.nStack
     for m in models:
         m.train()
     for e in models_ema:
         e.train()
+    runner = _StepGraph.get(_mt_ubpl_core, models, models_ema, optims, args)
     for bat, (augs_imgMap, augs_heatmaps, meta) in enumerate(trainLoader):
-        for o in optims:
-            o.zero_grad()
-        A = len(augs_imgMap)
-        imgs = [x.to(dev, non_blocking=True).float().contiguous() for x in augs_imgMap]
-        hms, gates = _targets(imgs, augs_heatmaps, meta, A, dev, args)
-        isl = _islabeled(meta["islabeled"][0], dev)
-        sw = _w(isl, 1.0, 0.0)                                   # getSampleWeight
-        nega = _w(isl, 0.0, args.pseudoWeight)                   # getSampleWeight_nega
-        B = imgs[0].shape[0]
-        outs, feats, outs_ema = [], [], []
-        mstreams = _ModelStreams.make(M, dev)
-        for mi in range(M):                                      # :228-243
-            oa, fa, ea = [], [], []
-            with (mstreams.on(mi) if mstreams else contextlib.nullcontext()):
-                for a in range(A):
-                    o, f = models[mi](imgs[a])
-                    oa.append(o)
-                    fa.append(f)
-            with (mstreams.on_teacher(mi) if mstreams else contextlib.nullcontext()):
-                for a in range(A):
-                    with torch.no_grad():
-                        ea.append(models_ema[mi](imgs[a])[0])
-            outs.append(oa)
-            feats.append(fa)
-            outs_ema.append(ea)
-        if mstreams:
-            mstreams.join([t for grp in (outs, feats, outs_ema) for ts in grp for t in ts])
-        K = outs[0][0].shape[2]
-        # ---- loss sums / counts on device
-        sums, cnts = [], []
-        ps_scores = []
-        for mi in range(M):
-            ms = []
-            for a in range(A):
-                s_d, _ = _dist_last(outs[mi][a], outs_ema[mi][a])
-                s_p, c_p = _mse(outs[mi][a], hms[a], S, gates[a], sw.reshape(-1, 1))
-                tg = torch.stack([outs_ema[j][a] for j in range(M)])
-                s_e, c_e, sc_e = _pseudo(outs[mi][a], tg, nega, S, args.pseudoScoreThr)
-                ms.append((s_d, s_p, c_p, s_e, c_e))
-                ps_scores.append(sc_e)
-            sums.append(ms)
-        fd = []
-        if args.FDLWeight > 0:
-            for a in range(A):                                   # :301-330 labeled rows
-                rowmask = _fdl_rows(sw, args)
-                v, c = features_cov(feats[0][a], feats[1][a], rowmask)
-                fd.append((v, c))
-        # pack: per model [mtc_sum, pec_sum, epc_sum], counts [pec_n, epc_n, n_sel] ; fdc
-        loc = []
-        cn = []
-        for mi in range(M):
-            loc += [sum(x[0] for x in sums[mi]), sum(x[1] for x in sums[mi]), sum(x[3] for x in sums[mi])]
-            cn += [sum(x[2][0] for x in sums[mi]), sum(x[4][1] for x in sums[mi]), sum(x[4][2] for x in sums[mi])]
-        if fd:
-            loc.append(sum(v for v, _ in fd))
-            cn.append(sum(c[0] for _, c in fd))
-        counts = torch.stack([c.float() for c in cn])
-        gcounts, gsums = _sync_stats(torch.stack([l.float() for l in loc]), counts)
-        W = D.world()
-        mtc_n = A * B * K * W
-        totals, rec = [], []
-        fdc = 0.
-        if fd:
-            fdc = args.FDLWeight * _norm(loc[-1], gcounts[-1])
-        for mi in range(M):
-            mtc = args.consWeight * (loc[3 * mi] / mtc_n)
-            pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[3 * mi])
-            epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[3 * mi + 1])
-            totals.append(pec + mtc + epc + fdc)
-            rec.append((pec, mtc, epc))
-        _backward_all(totals)                                     # :334-336
-        if mstreams:
-            mstreams.join()
-        D.allreduce_grads(models)
-        for o in optims:
-            o.step()
-        for mi, m in enumerate(models):
-            update_ema_variables(m, models_ema[mi], args)
-        # ---- records: one device->host copy
-        g_rec = []
-        for mi in range(M):
-            g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[3 * mi]),
-                      args.consWeight * gsums[3 * mi] / mtc_n,
-                      args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[3 * mi + 1])]
-        g_rec.append(args.FDLWeight * _norm(gsums[-1], gcounts[-1]) if fd else torch.zeros((), device=dev))
-        score = torch.stack(ps_scores).mean(0)
-        host = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, score]).cpu().tolist()
+        packed, (fd, mtc_n, B, ncn) = runner.run((augs_imgMap, augs_heatmaps, meta), dev)
+        host = packed.cpu().tolist()                              # the step's one device->host copy
         nrec = 3 * M + 1
         for mi in range(M):
             pec_c[mi].update(host[3 * mi], int(host[nrec + 3 * mi]))
@@ -302,12 +447,11 @@ def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
         if verbose:
             n_ps = int(sum(host[nrec + 3 * mi + 1] for mi in range(M)))
             n_sel = int(sum(host[nrec + 3 * mi + 2] for mi in range(M)))
-            sc = host[nrec + len(cn):]
+            sc = host[nrec + ncn:]
             print("batch.{} (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
                 format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
                 format(n_sel / n_ps if n_ps else float("nan"), ".2f"), format(n_sel, "5d"), format(n_ps, "5d"),
                 ", ".join(format(v, ".3f") for v in sc)))
-        del outs, outs_ema, feats, totals
     return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
 
 
