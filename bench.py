@@ -36,6 +36,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "images/sec training step (MT_UBPL, 2-stack HG, 256×256) at 1/2/4/8 GPUs; PCK@0.2"
 MEANS = [0.4920829, 0.4920829, 0.4920829]
 F32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+SPLIT6_PEAK_TFLOPS = 2500.0 / 6       # bf16 dense peak / 6 piece products per f32 product
 
 
 def make_args(B):
@@ -68,18 +69,37 @@ def make_batches(n, B, K, dev, seed):
 
 
 class ConvTimer:
-    """Wraps kernels.conv2d_forward: HIP events around every 3x3 forward launch
-    (on the current stream, which the kernel is launched on)."""
+    """HIP events around every launch of the dominant kernel — the Residual conv2
+    forward (3x3, fused BN+ReLU operand) — on the current stream, which the
+    kernel is launched on.  Precision 'f32': kernels.conv2d_forward
+    (conv_fwd_kernel, exact-f32 MFMA); '6xbf16': kernels.conv2d_forward_psa
+    (conv_psa_kernel, split-bf16 MFMA; its BN+ReLU+split pass is a separate
+    kernel and not part of the timed launch)."""
 
     def __init__(self, Kn):
         self.Kn = Kn
         self.orig = Kn.conv2d_forward
+        self.orig_psa = Kn.conv2d_forward_psa
         self.events = []
         self.flops = 0
         self.active = False
+        self.kind = None
 
     def __enter__(self):
-        orig = self.orig
+        orig, orig_psa = self.orig, self.orig_psa
+
+        def wrapped_psa(xs, ws, bias, res=None, out=None):
+            if not self.active or ws.shape[1] != 9 or bias is None:
+                return orig_psa(xs, ws, bias, res, out)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            y = orig_psa(xs, ws, bias, res, out)
+            e.record()
+            self.events.append((s, e))
+            self.kind = "psa"
+            self.flops += 2 * xs.B * ws.shape[0] * xs.C * 9 * xs.H * xs.W
+            return y
+        self.Kn.conv2d_forward_psa = wrapped_psa
 
         def wrapped(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out=None, w_tap=None):
             if not self.active or w is None or w.shape[-1] != 3 or pscale is None:
@@ -89,6 +109,7 @@ class ConvTimer:
             y = orig(x, w, bias, stride, pscale, pshift, res, out, w_tap)
             e.record()
             self.events.append((s, e))
+            self.kind = "f32"
             B, Cin = x.shape[:2]
             Cout = w.shape[0]
             self.flops += 2 * B * Cout * Cin * 9 * y.shape[-1] * y.shape[-2]
@@ -98,6 +119,7 @@ class ConvTimer:
 
     def __exit__(self, *a):
         self.Kn.conv2d_forward = self.orig
+        self.Kn.conv2d_forward_psa = self.orig_psa
 
     def result(self):
         torch.cuda.synchronize()
@@ -108,18 +130,24 @@ class ConvTimer:
         avg_ms = ms / n
         flops_per_launch = self.flops / n
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
-        return {"bound": "mfma", "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": (pmc_traffic() or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc_traffic(),
-                "kernel": "conv_fwd_kernel<3x3,f32 MFMA> (Residual conv2)", "launches": n,
+        if self.kind == "psa":
+            peak, kernel = SPLIT6_PEAK_TFLOPS, ("conv_psa_kernel<3x3, 6xbf16 split-f32 MFMA> (Residual conv2); "
+                                                "achieved/peak in f32-equivalent FLOP/s, peak = bf16 dense / 6")
+        else:
+            peak, kernel = F32_MFMA_PEAK_TFLOPS, "conv_fwd_kernel<3x3,f32 MFMA> (Residual conv2)"
+        pmc = pmc_traffic(self.kind)
+        return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "traffic": (pmc or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc,
+                "kernel": kernel, "launches": n,
                 "avg_launch_us": round(avg_ms * 1e3, 2), "flops_per_launch": int(flops_per_launch)}
 
 
-def pmc_traffic():
+def pmc_traffic(kind):
     """HBM bytes per launch of the roofline kernel, measured by rocprofv3 --pmc
     passes over this bench command (tools/gpu_pmc.sh bench ->
-    tools/pmc_roofline.py -> profiles/pmc_roofline.json); None if absent."""
-    p = os.path.join(ROOT, "profiles", "pmc_roofline.json")
+    tools/pmc_roofline.py -> profiles/pmc_roofline[_psa].json); None if absent."""
+    p = os.path.join(ROOT, "profiles", "pmc_roofline_psa.json" if kind == "psa" else "pmc_roofline.json")
     if not os.path.exists(p):
         return None
     with open(p) as fh:
@@ -250,6 +278,7 @@ def main():
             "metric": METRIC, "value": round(images / dt, 3), "unit": "images/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "conv_precision": Kn.conv_precision_name(),
             "data": "synthetic (U[0,1) images - means, integer keypoints, half labeled; heatmaps rendered on device)",
             "config": {"workload": "MT_UBPL train step, 2 students + 2 EMA teachers, 2 views",
                        "model": "StackedHourglass HG2 (K=16, AvgPool features)", "global_batch": B * world,

@@ -132,6 +132,33 @@ int ubpl_conv_weight_flip(const float* w, int Cout, int Cin, int KS, float* wt, 
  * (src_off, dst_off, Cout, Cin, KS*KS) in floats; mode 0 tap-major, 1 dgrad. */
 int ubpl_conv_weights_relayout(const float* src, float* dst, const int64_t* table, int nseg, int mode, void* stream);
 
+/* Split-bf16 MFMA path of the same Conv (conv_split.hip): every f32 operand
+ * carried as npieces (2 or 3) bf16 pieces, the piece products with
+ * pa + pb < npieces summed by v_mfma_f32_32x32x16_bf16 in f32.  Weights:
+ * ubpl_conv_weights_split writes npieces bf16 planes (`plane` elements apart)
+ * of the mode-0 (forward, grouped tap-major) or mode-1 (data-gradient) layout
+ * for many convs in one launch (table as above, dst_off % 8 == 0).
+ * ubpl_conv2d_forward_split: (KS, stride) in {(1,1), (3,1)}, Cin % 16 == 0,
+ * wsplit 16-B aligned; other arguments as ubpl_conv2d_forward. */
+int ubpl_conv_weights_split(const float* src, uint16_t* dst, int64_t plane, const int64_t* table, int nseg, int mode,
+                            int npieces, void* stream);
+int64_t ubpl_conv2d_forward_split_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo, int npieces);
+int ubpl_conv2d_forward_split(const float* x, int B, int Cin, int H, int W, const uint16_t* wsplit, int64_t plane,
+                              const float* bias, int Cout, int KS, int stride, const float* pscale,
+                              const float* pshift, const float* res, float* y, int Ho, int Wo, float* slab,
+                              int npieces, void* stream);
+/* Pre-split activations ("PSA"): npieces bf16 planes (`plane` elements apart)
+ * of [B][C/16][H+2pad][W+2pad][16] holding relu(x*pscale + pshift) (or x when
+ * pscale is null) with a zero border; C % 16 == 0. */
+int ubpl_split_activation(const float* x, int B, int C, int H, int W, const float* pscale, const float* pshift,
+                          int pad, int npieces, uint16_t* dst, int64_t plane, void* stream);
+/* Stride-1 conv (KS 1 or 3) of PSA activations (pad >= (KS-1)/2) with split
+ * weights: both operands DMA'd global -> LDS; y = conv + bias (+ res, may alias y). */
+int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int KS, int H, int W, int npieces);
+int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
+                            const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
+                            const float* res, float* y, float* slab, int npieces, void* stream);
+
 /* MaxPool2d(2,2) (models/base/layers.py:93), Upsample(x2, nearest) + add
  * (layers.py:110-111), AvgPool2d(2,2) projection (models/pose/hourglass.py:226). */
 int ubpl_maxpool2x2_forward(const float* x, int64_t planes, int H, int W, float* y, void* stream);

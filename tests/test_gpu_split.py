@@ -1,0 +1,161 @@
+"""Split-bf16 MFMA convolutions (conv_split.hip) vs float64 references.
+
+The exact-f32 MFMA path (conv.hip) is the yardstick: on the same inputs the
+3-piece path (npieces=3, "fp32-equivalent") must land within 2x the f32
+path's own error against float64, and the 2-piece path within the bound its
+arithmetic allows (operands carried to ~2^-16 relative: relative L2 of a
+layer's output <= 4e-5).  Weight re-layout, prologue, padding, residual,
+split-K and the data-gradient layout are all exercised.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ubpl_amd import _lib
+    _lib.load()
+
+
+def _rel(a, ref):
+    a = a.detach().cpu().double()
+    return float((a - ref).norm() / ref.norm())
+
+
+# (B, Cin, H, Cout, KS, prologue, residual): the hourglass shapes (1x1 and 3x3
+# at the large and the split-K-sized planes, Cout 16 / 64 / 128 / 256)
+CASES = [
+    (2, 128, 64, 128, 3, True, False),
+    (4, 128, 8, 128, 3, True, False),     # small grid: split-K + reduce
+    (2, 64, 32, 64, 3, True, False),
+    (2, 256, 16, 128, 1, True, False),
+    (2, 128, 16, 256, 1, True, True),
+    (2, 256, 64, 16, 1, False, False),    # preds head (Cout 16)
+    (2, 16, 32, 256, 1, False, True),     # merge_preds (Cin 16)
+    (3, 256, 4, 256, 1, True, True),
+]
+
+
+@pytest.mark.parametrize("npieces", [2, 3])
+@pytest.mark.parametrize("case", CASES)
+def test_split_forward_and_dgrad_vs_f64(case, npieces):
+    from ubpl_amd import kernels as Kn
+    B, Cin, H, Cout, KS, pro, resid = case
+    gen = torch.Generator().manual_seed(11 + hash(case) % 1000)
+    x = torch.randn(B, Cin, H, H, generator=gen, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, KS, KS, generator=gen, dtype=torch.float64) / np.sqrt(Cin * KS * KS)
+    b = torch.randn(Cout, generator=gen, dtype=torch.float64)
+    sc = torch.rand(Cin, generator=gen, dtype=torch.float64) + 0.5
+    sh = torch.randn(Cin, generator=gen, dtype=torch.float64) * 0.5
+    res = torch.randn(B, Cout, H, H, generator=gen, dtype=torch.float64) if resid else None
+    # the f32 inputs both paths see, and the float64 result on exactly those
+    x32, w32, b32, sc32, sh32 = (t.float() for t in (x, w, b, sc, sh))
+    res32 = res.float() if resid else None
+    inp = F.relu(x32.double() * sc32.double()[None, :, None, None] + sh32.double()[None, :, None, None]) if pro \
+        else x32.double()
+    yref = F.conv2d(inp, w32.double(), b32.double(), 1, (KS - 1) // 2)
+    if resid:
+        yref = yref + res32.double()
+    d = lambda t: None if t is None else t.to(DEV)
+    ps, ph = (d(sc32), d(sh32)) if pro else (None, None)
+    y_f32 = Kn.conv2d_forward(d(x32), d(w32), d(b32), 1, ps, ph, res=d(res32))
+    ws = Kn.conv_weight_split(d(w32), 0, npieces)
+    y_sp = Kn.conv2d_forward_split(d(x32), ws, d(b32), ps, ph, res=d(res32))
+    e32, esp = _rel(y_f32, yref), _rel(y_sp, yref)
+    print("fwd %s np=%d: f32 %.2e split %.2e" % (case, npieces, e32, esp))
+    if npieces == 3:
+        assert esp <= 2 * e32 + 1e-8, (esp, e32)
+    else:
+        assert esp <= 4e-5, (esp, e32)
+    # data gradient: dx = conv(dy, flip(w)^T) through the mode-1 split layout
+    dy = torch.randn(B, Cout, H, H, generator=gen, dtype=torch.float64).float()
+    dxref = torch.nn.grad.conv2d_input((B, Cin, H, H), w32.double(), dy.double(), 1, (KS - 1) // 2)
+    wd = Kn.conv_weight_split(d(w32), 1, npieces)
+    dx_sp = Kn.conv2d_forward_split(d(dy), wd, None)
+    dx_f32 = Kn.conv2d_dgrad(d(dy), d(w32))
+    e32, esp = _rel(dx_f32, dxref), _rel(dx_sp, dxref)
+    print("dgrad %s np=%d: f32 %.2e split %.2e" % (case, npieces, e32, esp))
+    if npieces == 3:
+        assert esp <= 2 * e32 + 1e-8, (esp, e32)
+    else:
+        assert esp <= 4e-5, (esp, e32)
+
+
+def test_split_weights_reconstruct():
+    """The pieces sum back to the f32 weight: exactly for 3 pieces, to ~2^-16 for 2."""
+    from ubpl_amd import kernels as Kn
+    gen = torch.Generator().manual_seed(3)
+    w = torch.randn(32, 16, 3, 3, generator=gen)
+    for npieces in (2, 3):
+        ws = Kn.conv_weight_split(w.to(DEV), 0, npieces)
+        planes = ws.buf.view(npieces, ws.plane)[:, :w.numel()].cpu()
+        f = lambda p: (planes[p].to(torch.int32) << 16).view(torch.float32)
+        tot = sum(f(p).double() for p in range(npieces))
+        # grouped tap-major order: wt[co][ci/16][tap][ci%16]
+        ref = w.reshape(32, 1, 16, 9).permute(0, 1, 3, 2).reshape(-1).double()
+        err = float((tot - ref).abs().max() / ref.abs().max())
+        assert err <= (0.0 if npieces == 3 else 2.0 ** -15), (npieces, err)
+
+
+@pytest.mark.parametrize("npieces", [3])
+@pytest.mark.parametrize("case", CASES)
+def test_psa_forward_and_dgrad_vs_f64(case, npieces):
+    """Pre-split activations (fused BN+ReLU+split pass) + LDS-DMA conv: same bar
+    as the register-staged split path."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, H, Cout, KS, pro, resid = case
+    gen = torch.Generator().manual_seed(23 + hash(case) % 1000)
+    x32 = torch.randn(B, Cin, H, H, generator=gen)
+    w32 = torch.randn(Cout, Cin, KS, KS, generator=gen) / np.sqrt(Cin * KS * KS)
+    b32 = torch.randn(Cout, generator=gen)
+    sc32 = torch.rand(Cin, generator=gen) + 0.5
+    sh32 = torch.randn(Cin, generator=gen) * 0.5
+    res32 = torch.randn(B, Cout, H, H, generator=gen) if resid else None
+    inp = F.relu(x32.double() * sc32.double()[None, :, None, None] + sh32.double()[None, :, None, None]) if pro \
+        else x32.double()
+    yref = F.conv2d(inp, w32.double(), b32.double(), 1, (KS - 1) // 2)
+    if resid:
+        yref = yref + res32.double()
+    d = lambda t: None if t is None else t.to(DEV)
+    ps, ph = (d(sc32), d(sh32)) if pro else (None, None)
+    y_f32 = Kn.conv2d_forward(d(x32), d(w32), d(b32), 1, ps, ph, res=d(res32))
+    for pad in sorted({(KS - 1) // 2, 1}):
+        xs = Kn.split_activation(d(x32), npieces, pad, ps, ph)
+        ws = Kn.conv_weight_split(d(w32), 0, npieces)
+        y_sp = Kn.conv2d_forward_psa(xs, ws, d(b32), res=d(res32))
+        e32, esp = _rel(y_f32, yref), _rel(y_sp, yref)
+        print("psa fwd %s pad=%d: f32 %.2e split %.2e" % (case, pad, e32, esp))
+        assert esp <= 2 * e32 + 1e-8, (esp, e32)
+    dy = torch.randn(B, Cout, H, H, generator=gen)
+    dxref = torch.nn.grad.conv2d_input((B, Cin, H, H), w32.double(), dy.double(), 1, (KS - 1) // 2)
+    ys = Kn.split_activation(d(dy), npieces, (KS - 1) // 2)
+    wd = Kn.conv_weight_split(d(w32), 1, npieces)
+    dx_sp = Kn.conv2d_forward_psa(ys, wd, None)
+    dx_f32 = Kn.conv2d_dgrad(d(dy), d(w32))
+    e32, esp = _rel(dx_f32, dxref), _rel(dx_sp, dxref)
+    print("psa dgrad %s: f32 %.2e split %.2e" % (case, e32, esp))
+    assert esp <= 2 * e32 + 1e-8, (esp, e32)
+
+
+def test_split_activation_layout():
+    """PSA image: pieces sum back to relu(x*s+h) exactly, border zero, [B][C/16][Hp][Wp][16]."""
+    from ubpl_amd import kernels as Kn
+    gen = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 32, 5, 7, generator=gen)
+    sc, sh = torch.rand(32, generator=gen) + 0.5, torch.randn(32, generator=gen)
+    xs = Kn.split_activation(x.to(DEV), 3, 1, sc.to(DEV), sh.to(DEV))
+    planes = xs.buf.view(3, xs.plane).cpu()
+    f = lambda p: (planes[p].to(torch.int32) << 16).view(torch.float32).double()
+    tot = (f(0) + f(1) + f(2)).view(2, 2, 7, 9, 16)
+    # fmaf(x, s, h) = the f64 value of x*s + h rounded once to f32
+    v = F.relu((x.double() * sc.double()[None, :, None, None] + sh.double()[None, :, None, None]).float()).double()
+    ref = torch.zeros(2, 2, 7, 9, 16, dtype=torch.float64)
+    ref[:, :, 1:6, 1:8, :] = v.view(2, 2, 16, 5, 7).permute(0, 1, 3, 4, 2)
+    assert torch.equal(tot, ref)

@@ -7,7 +7,11 @@ bench.py's ConvTimer.  Bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are KiB; gfx950's FETCH_SIZE counts half the bytes of wide reads,
 so it is doubled.  Writes profiles/pmc_roofline.json for bench.py.
 
-    python tools/pmc_roofline.py gpurun_out/pmc_bench profiles/pmc_roofline.json [source-tag]
+    python tools/pmc_roofline.py gpurun_out/pmc_bench profiles/pmc_roofline.json [source-tag] [f32|psa]
+
+With "psa" (conv precision 6xbf16) the roofline kernel is conv_psa_kernel<BM, 3, 3>:
+every 3x3 launch of it, forward and data gradient (same shapes, same traffic
+model; rocprof names cannot tell them apart).
 """
 import csv
 import json
@@ -15,7 +19,9 @@ import os
 import re
 import sys
 
-PAT = re.compile(r"conv_fwd_kernel<(\d+), 128, 3, 1, true, false")
+PATS = {"f32": re.compile(r"conv_fwd_kernel<(\d+), 128, 3, 1, true, false"),
+        "psa": re.compile(r"conv_psa_kernel<(\d+), 3, 3>")}
+PAT = PATS["f32"]
 
 
 def per_launch(path, counter):
@@ -31,12 +37,16 @@ def main():
     d = sys.argv[1]
     out = sys.argv[2]
     tag = sys.argv[3] if len(sys.argv) > 3 else d
+    kind = sys.argv[4] if len(sys.argv) > 4 else "f32"
+    global PAT
+    PAT = PATS[kind]
     fetch = per_launch(os.path.join(d, "fetch_counter_collection.csv"), "FETCH_SIZE")
     write = per_launch(os.path.join(d, "write_counter_collection.csv"), "WRITE_SIZE")
     nf, nw = len(fetch), len(write)
     fb = 2 * 1024 * sum(fetch.values()) / max(nf, 1)
     wb = 1024 * sum(write.values()) / max(nw, 1)
-    res = {"kernel": "conv_fwd_kernel<*,128,3,1,PRO> (all launches of the bench step)",
+    res = {"kernel": ("conv_fwd_kernel<*,128,3,1,PRO> (all launches of the bench step)" if kind == "f32" else
+                      "conv_psa_kernel<*,3,3> (all 3x3 launches of the bench step: forward + data gradient)"),
            "launches_fetch_pass": nf, "launches_write_pass": nw,
            "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
            "hbm_bytes_per_launch": fb + wb,

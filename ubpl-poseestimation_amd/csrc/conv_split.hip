@@ -1,0 +1,844 @@
+// Convolutions on the bf16 matrix cores with fp32 operands carried as sums of
+// bf16 pieces ("split-bf16"): v = v0 + v1 (+ v2), v0 = bf16(v), v1 = bf16(v - v0),
+// v2 = bf16(v - v0 - v1).  A product a*b is the sum of the piece products with
+// pa + pb < NP (the dropped ones are below the fp32-relevant range for NP = 3,
+// ~2^-16 relative for NP = 2), each exact in f32, summed by
+// v_mfma_f32_32x32x16_bf16 into an f32 accumulator:
+//   NP = 2: 3 MFMAs per 32x32x16 step (16/3 = 5.3x the v_mfma_f32_32x32x2_f32 rate);
+//   NP = 3: 6 MFMAs (2.7x), rounding error at the level of an f32 fmaf chain.
+// Same GEMM views, K order and epilogues as conv.hip (the Conv wrapper,
+// models/base/layers.py:31-50): grouped tap-major k = (ci/16)*16T + tap*16 + ci%16.
+//
+// Operand images in LDS: [piece][row][4 x 16 B] with the row's 32 k of one
+// K step in four 16-B chunks (chunk c = 2s + h holds k = 16s + 8h .. +7, the
+// 8 bf16 lane (r, h) of MFMA k-step s reads) — A rows = output channels, B rows
+// = output pixels n, both k-contiguous, chunk XOR-swizzled by (row >> 2) & 3
+// (conflict-free ds_read_b128 for the 16-lane groups of a 32-row fragment read).
+// Weights are split once per pass (ubpl_conv_weights_split, a batched
+// re-layout into NP bf16 planes); activations are split while they are staged,
+// after the fused BN+ReLU prologue.
+#include "common.h"
+using ubpl::xcd_remap;
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int BK = 32;
+constexpr int BN = 128;
+
+// Two floats -> NP packed bf16 pairs (piece p of a in the low half).
+template <int NP>
+__device__ __forceinline__ void split2(float a, float b, uint32_t (&o)[NP]) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const __bf16 ha = (__bf16)a, hb = (__bf16)b;
+        const bf16x2 v = {ha, hb};
+        o[p] = __builtin_bit_cast(uint32_t, v);
+        if (p + 1 < NP) {
+            a -= (float)ha;
+            b -= (float)hb;
+        }
+    }
+}
+
+__device__ __forceinline__ int swz(int row, int c) { return c ^ ((row >> 2) & 3); }
+
+// acc += sum over piece pairs (pa, pb), pa + pb < NP, smallest terms first
+template <int NP>
+__device__ __forceinline__ void mfma_split(floatx16& acc, const bf16x8 (&a)[NP], const bf16x8 (&b)[NP]) {
+#pragma unroll
+    for (int d = NP - 1; d >= 0; --d)
+#pragma unroll
+        for (int pa = d; pa >= 0; --pa) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa], b[d - pa], acc, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------ forward
+// x NCHW f32; wp: NP planes (stride wplane elements) of the grouped tap-major
+// weights [Cout][Ktot] as bf16; Cin % 16 == 0.  Epilogue / split-K slab as
+// conv.hip's conv_fwd_kernel.
+template <int BM, int KS, int ST, bool PRO, int NP>
+__global__ void __launch_bounds__(NT, 2) conv_fwd_split_kernel(
+    const float* __restrict__ x, const uint16_t* __restrict__ wp, int64_t wplane, const float* __restrict__ bias,
+    const float* __restrict__ pscale, const float* __restrict__ pshift, const float* res, float* y, int B, int Cin,
+    int H, int W, int Cout, int Ho, int Wo, int kchunk, float* __restrict__ slab) {
+    constexpr int PADK = (KS - 1) / 2;
+    constexpr int T = KS * KS;
+    constexpr int TM = BM / 64, TN = BN / 64;
+    constexpr int ACH = BM == 128 ? 2 : 1;   // 16-B weight chunks per thread per piece
+    __shared__ uint4 lds[2 * NP * (BM + BN) * 4];
+    uint4* As = lds;
+    uint4* Bs = lds + 2 * NP * BM * 4;
+
+    const int P = Ho * Wo, HWin = H * W;
+    const int64_t N = (int64_t)B * P;
+    const int Ktot = Cin * T;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                              gridDim.x * gridDim.y * gridDim.z);
+    const int by = lam % gridDim.y, bx = (lam / gridDim.y) % gridDim.x, bz = lam / (gridDim.y * gridDim.x);
+    const int m0 = by * BM;
+    const int64_t n0 = (int64_t)bx * BN;
+    const int k_begin = bz * kchunk;
+    const int k_end = min(Ktot, k_begin + kchunk);
+
+    // ---- A (weights) loader: row am, chunks ac0 .. ac0 + ACH - 1
+    const int am = tid % BM;
+    const int ac0 = (tid / BM) * ACH;
+    const bool am_ok = m0 + am < Cout;
+    const uint16_t* wrow = wp + (int64_t)min(m0 + am, Cout - 1) * Ktot;
+    // ---- B (activations) loader: column bn, k half g (16 k = one (group, tap))
+    const int bnl = tid & (BN - 1);
+    const int g = __builtin_amdgcn_readfirstlane(tid >> 7);
+    int cb = 0, coh = 0, cow = 0;
+    const int64_t ncol = n0 + bnl;
+    const bool cvalid = ncol < N;
+    if (cvalid) {
+        cb = (int)(ncol / P);
+        const int p = (int)(ncol - (int64_t)cb * P);
+        coh = p / Wo;
+        cow = p - coh * Wo;
+    }
+    const float* xb = x + (int64_t)cb * Cin * HWin;
+
+    uint4 ra[NP][ACH];
+    float rb[16];
+    bool b_inb = false;
+
+    auto load = [&](int kt) {
+        {
+            const int k = min(kt + 8 * ac0, Ktot - 8 * ACH);
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+#pragma unroll
+                for (int c = 0; c < ACH; ++c)
+                    ra[p][c] = *reinterpret_cast<const uint4*>(wrow + (int64_t)p * wplane + k + 8 * c);
+        }
+        const int kk = kt + 16 * g;
+        const int kg = kk >> 4;
+        const int tap = kg % T;
+        const int ci0 = min((kg / T) * 16, Cin - 16);
+        const int kh = tap / KS, kw = tap - kh * KS;
+        const int ih = coh * ST - PADK + kh, iw = cow * ST - PADK + kw;
+        b_inb = cvalid && kk < k_end && ih >= 0 && ih < H && iw >= 0 && iw < W;
+        const float* src = xb + (int64_t)ci0 * HWin + (b_inb ? ih * W + iw : 0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) rb[j] = src[(int64_t)j * HWin];
+    };
+    auto store = [&](int buf, int kt) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int c = 0; c < ACH; ++c) {
+                const int ch = ac0 + c;
+                const bool ok = am_ok && kt + 8 * ch < k_end;
+                As[((buf * NP + p) * BM + am) * 4 + swz(am, ch)] = ok ? ra[p][c] : make_uint4(0, 0, 0, 0);
+            }
+        // prologue on every element (unconditional scalar loads of the 16
+        // channels' coefficients), then a select: a load or an LDS read under
+        // the in-bounds condition becomes a branch with its own vmcnt(0)
+        float v[16];
+        if (PRO) {
+            const int kg = (kt + 16 * g) >> 4;
+            const int ci0 = __builtin_amdgcn_readfirstlane(min((kg / T) * 16, Cin - 16));
+            float sc[16], sh[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                sc[j] = pscale[ci0 + j];
+                sh[j] = pshift[ci0 + j];
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = fmaxf(fmaf(rb[j], sc[j], sh[j]), 0.f);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = rb[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = b_inb ? v[j] : 0.f;
+        uint32_t pk[NP][8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            uint32_t o[NP];
+            split2<NP>(v[2 * i], v[2 * i + 1], o);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) pk[p][i] = o[p];
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            uint4* rowp = Bs + ((buf * NP + p) * BN + bnl) * 4;
+            rowp[swz(bnl, 2 * g)] = make_uint4(pk[p][0], pk[p][1], pk[p][2], pk[p][3]);
+            rowp[swz(bnl, 2 * g + 1)] = make_uint4(pk[p][4], pk[p][5], pk[p][6], pk[p][7]);
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nkt = (k_end - k_begin + BK - 1) / BK;
+    if (nkt > 0) {
+        load(k_begin);
+        store(0, k_begin);
+    }
+    if (nkt > 1) load(k_begin + BK);
+    const int li = lane & 31, h = lane >> 5;
+    for (int t = 0; t < nkt; ++t) {
+        const int cur = t & 1;
+        __syncthreads();
+        if (t + 1 < nkt) {
+            store(cur ^ 1, k_begin + (t + 1) * BK);
+            if (t + 2 < nkt) load(k_begin + (t + 2) * BK);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int c = 2 * s + h;
+            bf16x8 af[TM][NP], bfr[TN][NP];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int row = wm + 32 * i + li;
+#pragma unroll
+                for (int p = 0; p < NP; ++p)
+                    af[i][p] = __builtin_bit_cast(bf16x8, As[((cur * NP + p) * BM + row) * 4 + swz(row, c)]);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int row = wn + 32 * j + li;
+#pragma unroll
+                for (int p = 0; p < NP; ++p)
+                    bfr[j][p] = __builtin_bit_cast(bf16x8, Bs[((cur * NP + p) * BN + row) * 4 + swz(row, c)]);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    if constexpr (NP == 3) {
+                        // the bf16 MFMA aligns its 17 addends to the largest and
+                        // truncates below ~2^-26 of it (tools/experiments/mfma_numerics):
+                        // against a large running sum that bias grows with K.  Each
+                        // 16-k chunk starts from 0 and is added with a rounded f32 add.
+                        floatx16 tmp;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) tmp[r] = 0.f;
+                        mfma_split<NP>(tmp, af[i], bfr[j]);
+                        acc[i][j] += tmp;
+                    } else {
+                        mfma_split<NP>(acc[i][j], af[i], bfr[j]);
+                    }
+                }
+        }
+    }
+
+    if (slab != nullptr) {
+        float* sl = slab + (int64_t)bz * Cout * N;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int64_t n = n0 + wn + 32 * j + li;
+            if (n >= N) continue;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (m < Cout) sl[(int64_t)m * N + n] = acc[i][j][r];
+                }
+        }
+        return;
+    }
+    // epilogue: + bias (+ residual; res may alias y: all loads before any store)
+    int64_t obase[TN];
+    bool nok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn + 32 * j + li;
+        nok[j] = n < N;
+        const int64_t nc = nok[j] ? n : N - 1;
+        const int b = (int)(nc / P);
+        const int p = (int)(nc - (int64_t)b * P);
+        obase[j] = (int64_t)b * Cout * P + p;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, Cout - 1);
+                if (bias) acc[i][j][r] += bias[m];
+                if (res) acc[i][j][r] += res[obase[j] + (int64_t)m * P];
+            }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        if (!nok[j]) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < Cout) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+            }
+    }
+}
+
+// ------------------------------------------------------------------ pre-split activations
+// PSA layout: NP bf16 planes (`plane` elements apart) of [B][C/16][Hp][Wp][16],
+// Hp = H + 2*pad, Wp = W + 2*pad, the border zero: a pixel's 16 channels of one
+// group are 32 contiguous bytes = the two 16-B chunks of one B-operand row of
+// a K step, and a 3x3 tap is a constant offset (no bounds checks in the conv).
+// v = relu(x*scale + shift) (PRO) or x, then split; the border stays 0 (the
+// reference pads the BN+ReLU output: models/base/layers.py:45-50).
+template <int NP, bool PRO>
+__global__ void __launch_bounds__(256) split_act_kernel(const float* __restrict__ x, int C, int H, int W,
+                                                       const float* __restrict__ pscale,
+                                                       const float* __restrict__ pshift, int pad,
+                                                       uint16_t* __restrict__ dst, int64_t plane) {
+    const int Hp = H + 2 * pad, Wp = W + 2 * pad, G = C >> 4;
+    const int b = blockIdx.z, g = blockIdx.y;
+    const int pix = blockIdx.x * 256 + threadIdx.x;
+    if (pix >= Hp * Wp) return;
+    const int hp = pix / Wp, wq = pix - hp * Wp;
+    const int h = hp - pad, w = wq - pad;
+    const bool in = h >= 0 && h < H && w >= 0 && w < W;
+    const int64_t HW = (int64_t)H * W;
+    const float* src = x + ((int64_t)b * C + 16 * g) * HW + (in ? h * W + w : 0);
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = src[j * HW];
+    if (PRO) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = fmaxf(fmaf(v[j], pscale[16 * g + j], pshift[16 * g + j]), 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = in ? v[j] : 0.f;
+    uint32_t pk[NP][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t o[NP];
+        split2<NP>(v[2 * i], v[2 * i + 1], o);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) pk[p][i] = o[p];
+    }
+    uint16_t* d = dst + (((int64_t)(b * G + g) * Hp + hp) * Wp + wq) * 16;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        *reinterpret_cast<uint4*>(d + p * plane) = make_uint4(pk[p][0], pk[p][1], pk[p][2], pk[p][3]);
+        *reinterpret_cast<uint4*>(d + p * plane + 8) = make_uint4(pk[p][4], pk[p][5], pk[p][6], pk[p][7]);
+    }
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+// Forward conv (stride 1) over PSA activations and split weights, both staged
+// global -> LDS by LDS-DMA (global_load_lds_dwordx4: no staging registers, no
+// VALU), BK = 16 = one (channel group, tap) per K step.  LDS stage image:
+// [piece][row][2 x 16 B] for A (BM rows) then B (128 rows); a DMA instruction
+// fills 32 rows lane-linearly (lane L: row L>>1, slot L&1), so the chunk
+// swizzle c ^ ((row >> 3) & 1) (conflict-free ds_read_b128 of a 32-row
+// fragment) is applied on the SOURCE address and again on the read.  Wave w
+// moves rows 32w..32w+31 of both operands.  3-stage ring: stage t+2 is issued
+// right after the barrier that retires stage t (each wave's counted vmcnt
+// leaves stage t+1's DMA in flight; raw s_barrier, never __syncthreads, whose
+// fence would drain it: cdna_hip_programming.md §5 'Pipelining across barriers').
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int KS, int NP>
+__global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
+                                                        const uint16_t* __restrict__ wp, int64_t wplane,
+                                                        const float* __restrict__ bias, const float* res, float* y,
+                                                        int B, int Cin, int H, int W, int pad, int Cout, int kchunk,
+                                                        float* __restrict__ slab) {
+    constexpr int PADK = (KS - 1) / 2;
+    constexpr int T = KS * KS;
+    constexpr int TM = BM / 64, TN = BN / 64;
+    constexpr int AB = NP * BM * 32, BB = NP * BN * 32;   // bytes per stage
+    constexpr int NS = 3;
+    __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
+
+    const int P = H * W, Hp = H + 2 * pad, Wp = W + 2 * pad, G = Cin >> 4;
+    const int64_t N = (int64_t)B * P;
+    const int Ktot = Cin * T;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                              gridDim.x * gridDim.y * gridDim.z);
+    const int by = lam % gridDim.y, bx = (lam / gridDim.y) % gridDim.x, bz = lam / (gridDim.y * gridDim.x);
+    const int m0 = by * BM;
+    const int64_t n0 = (int64_t)bx * BN;
+    const int k_begin = bz * kchunk;
+    const int k_end = min(Ktot, k_begin + kchunk);
+
+    // DMA lane geometry
+    const int lr = lane >> 1;
+    const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
+    const bool a_issue = wid < BM / 32;
+    const uint16_t* a_src = wp + (int64_t)min(m0 + 32 * wid + lr, Cout - 1) * Ktot + 8 * lchunk;
+    const uint16_t* b_src;
+    {
+        int64_t n = n0 + 32 * wid + lr;
+        n = n < N ? n : N - 1;
+        const int b = (int)(n / P);
+        const int p = (int)(n - (int64_t)b * P);
+        const int oh = p / W, ow = p - oh * W;
+        b_src = xs + (((int64_t)b * G * Hp + oh + pad - PADK) * Wp + ow + pad - PADK) * 16 + 8 * lchunk;
+    }
+    auto stage = [&](int buf, int kt) {
+        const int kg = kt >> 4;
+        const int tap = kg % T, cg = kg / T;
+        const int kh = tap / KS, kw = tap - kh * KS;
+        const int64_t boff = ((int64_t)cg * Hp + kh) * Wp * 16 + kw * 16;
+        char* base = lds + buf * (AB + BB);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if (a_issue)
+                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(a_src + p * wplane + kt),
+                                                 (lds_ptr_t)(base + p * BM * 32 + wid * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(b_src + p * xplane + boff),
+                                             (lds_ptr_t)(base + AB + p * BN * 32 + wid * 1024), 16, 0, 0);
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nkt = (k_end - k_begin) >> 4;
+    if (nkt > 0) stage(0, k_begin);
+    if (nkt > 1) stage(1, k_begin + 16);
+    const int li = lane & 31, h = lane >> 5;
+    for (int t = 0; t < nkt; ++t) {
+        // retire stage t (this wave's DMA), then the barrier: every wave's
+        // stage t has landed and every wave is done reading stage t-1
+        if (t + 1 < nkt) {
+            if (a_issue) vm_wait<2 * NP>();
+            else vm_wait<NP>();
+        } else {
+            vm_wait<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + 2 < nkt) stage((t + 2) % NS, k_begin + (t + 2) * 16);
+        const int cur = t % NS;
+        const char* base = lds + cur * (AB + BB);
+        bf16x8 af[TM][NP], bfr[TN][NP];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int row = wm + 32 * i + li;
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                af[i][p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int row = wn + 32 * j + li;
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                bfr[j][p] = *reinterpret_cast<const bf16x8*>(base + AB + p * BN * 32 + row * 32 +
+                                                            16 * (h ^ ((row >> 3) & 1)));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if constexpr (NP == 3) {
+                    floatx16 tmp;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) tmp[r] = 0.f;
+                    mfma_split<NP>(tmp, af[i], bfr[j]);
+                    acc[i][j] += tmp;
+                } else {
+                    mfma_split<NP>(acc[i][j], af[i], bfr[j]);
+                }
+            }
+        // fragments consumed (the MFMAs waited on them) before the next barrier
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    if (slab != nullptr) {
+        float* sl = slab + (int64_t)bz * Cout * N;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int64_t n = n0 + wn + 32 * j + li;
+            if (n >= N) continue;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (m < Cout) sl[(int64_t)m * N + n] = acc[i][j][r];
+                }
+        }
+        return;
+    }
+    int64_t obase[TN];
+    bool nok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn + 32 * j + li;
+        nok[j] = n < N;
+        const int64_t nc = nok[j] ? n : N - 1;
+        const int b = (int)(nc / P);
+        const int p = (int)(nc - (int64_t)b * P);
+        obase[j] = (int64_t)b * Cout * P + p;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, Cout - 1);
+                if (bias) acc[i][j][r] += bias[m];
+                if (res) acc[i][j][r] += res[obase[j] + (int64_t)m * P];
+            }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        if (!nok[j]) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < Cout) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+            }
+    }
+}
+
+// y[b,m,p] = sum_z slab[z][m][b*P+p] + bias[m] (+ res)
+__global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restrict__ slab, int splits, int Cout, int P,
+                                                          int64_t N, const float* __restrict__ bias, const float* res,
+                                                          float* y) {
+    const int64_t total = (int64_t)Cout * N;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(i % P);
+        const int64_t t = i / P;
+        const int m = (int)(t % Cout);
+        const int64_t b = t / Cout;
+        const int64_t n = b * P + p;
+        float s = 0.f;
+        for (int z = 0; z < splits; ++z) s += slab[((int64_t)z * Cout + m) * N + n];
+        if (bias) s += bias[m];
+        if (res) s += res[i];
+        y[i] = s;
+    }
+}
+
+// ------------------------------------------------------------------ weights
+// Batched split re-layout over a segment table (int64 [nseg][5]: src_off,
+// dst_off, Cout, Cin, T), one segment per blockIdx.y; NP bf16 planes of
+// `plane` elements.  mode 0: forward layout wt[co][ci/G][tap][ci%G] =
+// w[co][ci][tap]; mode 1: data-gradient layout wd[ci][co/G][tap][co%G] =
+// w[co][ci][T-1-tap] (G = 16 when it divides the contraction channels).
+__global__ void __launch_bounds__(256) split_relayout_kernel(const float* __restrict__ src,
+                                                            uint16_t* __restrict__ dst, int64_t plane,
+                                                            const int64_t* __restrict__ table, int mode, int np) {
+    const int64_t* e = table + (int64_t)blockIdx.y * 5;
+    const int64_t so = e[0], dof = e[1];
+    const int Cout = (int)e[2], Cin = (int)e[3], T = (int)e[4];
+    const int64_t total = (int64_t)Cout * Cin * T;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t s;
+        if (mode == 0) {
+            const int G = ubpl::conv_kgroup(Cin);
+            const int gi = (int)(i % G);
+            const int64_t t1 = i / G;
+            const int tap = (int)(t1 % T);
+            const int64_t t2 = t1 / T;
+            const int cbk = (int)(t2 % (Cin / G));
+            const int co = (int)(t2 / (Cin / G));
+            s = ((int64_t)co * Cin + cbk * G + gi) * T + tap;
+        } else {
+            const int G = ubpl::conv_kgroup(Cout);
+            const int gi = (int)(i % G);
+            const int64_t t1 = i / G;
+            const int tap = (int)(t1 % T);
+            const int64_t t2 = t1 / T;
+            const int cbk = (int)(t2 % (Cout / G));
+            const int ci = (int)(t2 / (Cout / G));
+            s = ((int64_t)(cbk * G + gi) * Cin + ci) * T + (T - 1 - tap);
+        }
+        float v = src[so + s];
+        for (int p = 0; p < np; ++p) {
+            const __bf16 hv = (__bf16)v;
+            dst[(int64_t)p * plane + dof + i] = __builtin_bit_cast(uint16_t, hv);
+            v -= (float)hv;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ planning
+struct Plan {
+    int bm, splits, kchunk;
+};
+
+struct Occ {
+    int ncu = 256;
+    int f128[2] = {2, 1}, f64[2] = {3, 2};   // register-staged kernel [NP == 3]
+    int p128[2] = {2, 2}, p64[2] = {3, 2};   // conv_psa_kernel [NP == 3]
+};
+
+const Occ& occ_info();
+
+// Blocks spread evenly over the CUs; a CU with c blocks (r = min(c, occ)
+// resident) runs them in c * (steps + 2) K steps at a rate that needs ~2
+// resident blocks to hide latency.  Split-K adds the slab round trip + a launch.
+double plan_cost(int64_t tiles, int s, int64_t nsteps, int occ, int ncu, double step_flops, double slab_bytes) {
+    const int64_t blocks = tiles * s;
+    const int64_t per_cu = (blocks + ncu - 1) / ncu;
+    const int64_t r = per_cu < occ ? per_cu : occ;
+    const double eff = r >= 2 ? 1.0 : 0.6;
+    const int64_t steps = (nsteps + s - 1) / s;
+    const double rate = 2.0e12;   // split-bf16 flop/s per CU, sustained (model only)
+    double t = (double)((per_cu + r - 1) / r) * r * (double)(steps + 2) * step_flops / (rate * eff);
+    if (s > 1) t += 2.0 * s * slab_bytes / 5e12 + 4e-6;
+    return t;
+}
+
+Plan fwd_plan(int Cout, int64_t N, int Ktot, int np, bool psa = false) {
+    const Occ& d = occ_info();
+    const int bk = psa ? 16 : BK;
+    const int nkt = (Ktot + bk - 1) / bk;
+    const int maxs = nkt / 2 > 0 ? nkt / 2 : 1;
+    Plan best{64, 1, 0};
+    double bc = 1e30;
+    for (int bm : {128, 64}) {
+        if (bm == 128 && Cout <= 64) continue;
+        const int64_t tiles = ((Cout + bm - 1) / bm) * ((N + BN - 1) / BN);
+        const int occ = psa ? (bm == 128 ? d.p128[np == 3] : d.p64[np == 3])
+                            : (bm == 128 ? d.f128[np == 3] : d.f64[np == 3]);
+        const double sf = 2.0 * bm * BN * bk;
+        int s_best = 1;
+        double c_best = plan_cost(tiles, 1, nkt, occ, d.ncu, sf, 4.0 * Cout * N);
+        for (int s = 2; s <= maxs; ++s) {
+            const double c = plan_cost(tiles, s, nkt, occ, d.ncu, sf, 4.0 * Cout * N);
+            if (c < c_best * 0.97) {
+                c_best = c;
+                s_best = s;
+            }
+        }
+        const double c = c_best / (bm == 128 ? 1.0 : 0.85);
+        if (c < bc) {
+            bc = c;
+            best.bm = bm;
+            best.splits = s_best;
+        }
+    }
+    const int steps = (nkt + best.splits - 1) / best.splits;
+    best.kchunk = steps * bk;
+    best.splits = (nkt + steps - 1) / steps;
+    return best;
+}
+
+void launch_split_reduce(const float* slab, int splits, int Cout, int P, int64_t N, const float* bias,
+                         const float* res, float* y, hipStream_t st);
+
+template <int BM, int KS, int NP>
+int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t wplane, const float* bias,
+               const float* res, float* y, int B, int Cin, int H, int W, int pad, int Cout, const Plan& pl,
+               float* slab, hipStream_t st) {
+    const int64_t N = (int64_t)B * H * W;
+    dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
+    const bool split = pl.splits > 1;
+    hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP>), grid, dim3(NT), 0, st, xs, xplane, wp, wplane, bias,
+                       split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr);
+    UBPL_LAUNCH_CHECK();
+    if (split) {
+        launch_split_reduce(slab, pl.splits, Cout, H * W, N, bias, res, y, st);
+        UBPL_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
+template <int BM, int KS, int ST, bool PRO, int NP>
+int launch_fwd(const float* x, const uint16_t* wp, int64_t plane, const float* bias, const float* ps, const float* sh,
+               const float* res, float* y, int B, int Cin, int H, int W, int Cout, int Ho, int Wo, const Plan& pl,
+               float* slab, hipStream_t st) {
+    const int64_t N = (int64_t)B * Ho * Wo;
+    dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
+    const bool split = pl.splits > 1;
+    hipLaunchKernelGGL((conv_fwd_split_kernel<BM, KS, ST, PRO, NP>), grid, dim3(NT), 0, st, x, wp, plane, bias, ps, sh,
+                       split ? nullptr : res, y, B, Cin, H, W, Cout, Ho, Wo, pl.kchunk, split ? slab : nullptr);
+    UBPL_LAUNCH_CHECK();
+    if (split) {
+        launch_split_reduce(slab, pl.splits, Cout, Ho * Wo, N, bias, res, y, st);
+        UBPL_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
+void launch_split_reduce(const float* slab, int splits, int Cout, int P, int64_t N, const float* bias,
+                         const float* res, float* y, hipStream_t st) {
+    const int64_t total = (int64_t)Cout * N;
+    int gsz = (int)((total + 255) / 256);
+    if (gsz > 8192) gsz = 8192;
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(gsz), dim3(256), 0, st, slab, splits, Cout, P, N, bias, res, y);
+}
+
+template <int KS, int ST, int NP>
+int fwd_dispatch(const Plan& pl, bool pro, const float* x, const uint16_t* wp, int64_t plane, const float* bias,
+                 const float* ps, const float* sh, const float* res, float* y, int B, int Cin, int H, int W, int Cout,
+                 int Ho, int Wo, float* slab, hipStream_t st) {
+#define UBPL_FS(BM_, PRO_)                                                                                        \
+    return launch_fwd<BM_, KS, ST, PRO_, NP>(x, wp, plane, bias, ps, sh, res, y, B, Cin, H, W, Cout, Ho, Wo, pl, \
+                                             slab, st)
+    if (pl.bm == 128) {
+        if (pro) UBPL_FS(128, true);
+        UBPL_FS(128, false);
+    }
+    if (pro) UBPL_FS(64, true);
+    UBPL_FS(64, false);
+#undef UBPL_FS
+}
+
+const Occ& occ_info() {
+    static Occ d = [] {
+        Occ r;
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+            r.ncu = v;
+        auto q = [&](const void* f, int& dst) {
+            int o = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, f, NT, 0) == hipSuccess && o > 0) dst = o;
+        };
+        q((const void*)conv_fwd_split_kernel<128, 3, 1, true, 2>, r.f128[0]);
+        q((const void*)conv_fwd_split_kernel<128, 3, 1, true, 3>, r.f128[1]);
+        q((const void*)conv_fwd_split_kernel<64, 3, 1, true, 2>, r.f64[0]);
+        q((const void*)conv_fwd_split_kernel<64, 3, 1, true, 3>, r.f64[1]);
+        q((const void*)conv_psa_kernel<128, 3, 2>, r.p128[0]);
+        q((const void*)conv_psa_kernel<128, 3, 3>, r.p128[1]);
+        q((const void*)conv_psa_kernel<64, 3, 2>, r.p64[0]);
+        q((const void*)conv_psa_kernel<64, 3, 3>, r.p64[1]);
+        (void)hipGetLastError();
+        return r;
+    }();
+    return d;
+}
+
+}  // namespace
+
+// Floats of split-K workspace ubpl_conv2d_forward_split needs; 0 = none.
+UBPL_API int64_t ubpl_conv2d_forward_split_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo, int npieces) {
+    const int64_t N = (int64_t)B * Ho * Wo;
+    const Plan pl = fwd_plan(Cout, N, Cin * KS * KS, npieces);
+    return pl.splits > 1 ? (int64_t)pl.splits * Cout * N : 0;
+}
+
+// y = conv(relu(x*pscale + pshift) or x, w, pad (KS-1)/2) + bias (+ res) on the
+// split-bf16 MFMA path.  wsplit: npieces (2 or 3) bf16 planes, `plane`
+// elements apart, of the weights in ubpl_conv_weights_split's layout.
+// (KS, stride) in {(1,1), (3,1)}; Cin % 16 == 0; res may alias y.
+UBPL_API int ubpl_conv2d_forward_split(const float* x, int B, int Cin, int H, int W, const uint16_t* wsplit,
+                                       int64_t plane, const float* bias, int Cout, int KS, int stride,
+                                       const float* pscale, const float* pshift, const float* res, float* y, int Ho,
+                                       int Wo, float* slab, int npieces, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (Cin % 16 != 0 || stride != 1 || (npieces != 2 && npieces != 3)) return (int)hipErrorInvalidValue;
+    if ((((uintptr_t)wsplit) & 15) != 0 || (plane % 8) != 0) return (int)hipErrorInvalidValue;
+    const bool pro = pscale != nullptr;
+    const int64_t N = (int64_t)B * Ho * Wo;
+    const Plan pl = fwd_plan(Cout, N, Cin * KS * KS, npieces);
+    if (pl.splits > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
+#define UBPL_FD(KS_, NP_)                                                                                     \
+    return fwd_dispatch<KS_, 1, NP_>(pl, pro, x, wsplit, plane, bias, pscale, pshift, res, y, B, Cin, H, W, \
+                                     Cout, Ho, Wo, slab, st)
+    if (KS == 1) {
+        if (npieces == 2) UBPL_FD(1, 2);
+        UBPL_FD(1, 3);
+    }
+    if (KS == 3) {
+        if (npieces == 2) UBPL_FD(3, 2);
+        UBPL_FD(3, 3);
+    }
+#undef UBPL_FD
+    return (int)hipErrorInvalidValue;
+}
+
+// Split re-layout of many convs in one launch (table as ubpl_conv_weights_relayout;
+// dst_off multiples of 8).  dst: npieces planes of `plane` bf16 elements.
+UBPL_API int ubpl_conv_weights_split(const float* src, uint16_t* dst, int64_t plane, const int64_t* table, int nseg,
+                                     int mode, int npieces, void* stream) {
+    if (nseg <= 0) return 0;
+    if (npieces < 1 || npieces > 3) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(split_relayout_kernel, dim3(64, nseg), dim3(256), 0, (hipStream_t)stream, src, dst, plane,
+                       table, mode, npieces);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// Pre-split activations (PSA layout, see split_act_kernel): dst = npieces bf16
+// planes `plane` elements apart of [B][C/16][H+2pad][W+2pad][16];
+// v = relu(x*pscale + pshift) when pscale != nullptr, else x.  C % 16 == 0.
+UBPL_API int ubpl_split_activation(const float* x, int B, int C, int H, int W, const float* pscale,
+                                   const float* pshift, int pad, int npieces, uint16_t* dst, int64_t plane,
+                                   void* stream) {
+    if (C % 16 != 0 || npieces < 2 || npieces > 3 || pad < 0 || (plane % 8) != 0) return (int)hipErrorInvalidValue;
+    const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+    dim3 grid((unsigned)((Hp * Wp + 255) / 256), (unsigned)(C / 16), (unsigned)B);
+    hipStream_t st = (hipStream_t)stream;
+    const bool pro = pscale != nullptr;
+#define UBPL_SA(NP_, PRO_)                                                                                      \
+    hipLaunchKernelGGL((split_act_kernel<NP_, PRO_>), grid, dim3(256), 0, st, x, C, H, W, pscale, pshift, pad, \
+                       dst, plane)
+    if (npieces == 2) {
+        if (pro) UBPL_SA(2, true);
+        else UBPL_SA(2, false);
+    } else {
+        if (pro) UBPL_SA(3, true);
+        else UBPL_SA(3, false);
+    }
+#undef UBPL_SA
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+UBPL_API int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int KS, int H, int W, int npieces) {
+    const int64_t N = (int64_t)B * H * W;
+    const Plan pl = fwd_plan(Cout, N, Cin * KS * KS, npieces, true);
+    return pl.splits > 1 ? (int64_t)pl.splits * Cout * N : 0;
+}
+
+// y = conv(xs, w, stride 1, pad (KS-1)/2) + bias (+ res) with xs in the PSA
+// layout (border pad >= (KS-1)/2) and w from ubpl_conv_weights_split (same
+// npieces).  KS in {1, 3}; Cin % 16 == 0; res may alias y.
+UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
+                                     const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
+                                     const float* res, float* y, float* slab, int npieces, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (Cin % 16 != 0 || (npieces != 2 && npieces != 3) || pad < (KS - 1) / 2) return (int)hipErrorInvalidValue;
+    if ((((uintptr_t)wsplit) & 15) != 0 || (((uintptr_t)xs) & 15) != 0 || (wplane % 8) != 0 || (xplane % 8) != 0)
+        return (int)hipErrorInvalidValue;
+    const int64_t N = (int64_t)B * H * W;
+    const Plan pl = fwd_plan(Cout, N, Cin * KS * KS, npieces, true);
+    if (pl.splits > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
+#define UBPL_PS(BM_, KS_, NP_) \
+    return launch_psa<BM_, KS_, NP_>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl, slab, st)
+#define UBPL_PS_BM(KS_, NP_)          \
+    if (pl.bm == 128) UBPL_PS(128, KS_, NP_); \
+    UBPL_PS(64, KS_, NP_)
+    if (KS == 1) {
+        if (npieces == 2) { UBPL_PS_BM(1, 2); }
+        UBPL_PS_BM(1, 3);
+    }
+    if (KS == 3) {
+        if (npieces == 2) { UBPL_PS_BM(3, 2); }
+        UBPL_PS_BM(3, 3);
+    }
+#undef UBPL_PS_BM
+#undef UBPL_PS
+    return (int)hipErrorInvalidValue;
+}

@@ -41,6 +41,12 @@ SIGNATURES = {
     "ubpl_conv2d_wgrad": (I, [P, P, I, I, I, I, I, I, I, P, P, I, I, P, P, P, I, P]),
     "ubpl_conv_weight_flip": (I, [P, I, I, I, P, P]),
     "ubpl_conv_weights_relayout": (I, [P, P, P, I, I, P]),
+    "ubpl_conv2d_forward_split_workspace": (L, [I, I, I, I, I, I, I]),
+    "ubpl_conv2d_forward_split": (I, [P, I, I, I, I, P, L, P, I, I, I, P, P, P, P, I, I, P, I, P]),
+    "ubpl_conv_weights_split": (I, [P, P, L, P, I, I, I, P]),
+    "ubpl_split_activation": (I, [P, I, I, I, I, P, P, I, I, P, L, P]),
+    "ubpl_conv2d_forward_psa_workspace": (L, [I, I, I, I, I, I, I]),
+    "ubpl_conv2d_forward_psa": (I, [P, L, I, I, I, I, I, P, L, P, I, I, P, P, P, I, P]),
     "ubpl_maxpool2x2_forward": (I, [P, L, I, I, P, P]),
     "ubpl_maxpool2x2_backward": (I, [P, P, L, I, I, P, I, P]),
     "ubpl_avgpool2x2_forward": (I, [P, L, I, I, P, P]),

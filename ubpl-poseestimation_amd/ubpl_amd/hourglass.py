@@ -180,20 +180,10 @@ class StackedHourglass(nn.Module):
         self._grad_views_attached = False
         self._ws = {}
         # re-laid-out conv weights, rebuilt by one launch per forward (tap-major
-        # [Cout][T][Cin] for KS > 1) and per backward (dgrad [Cin][T][Cout])
-        self._wlay = {}
-        for mode, keep in ((0, lambda ks, nm: ks > 1), (1, lambda ks, nm: nm != "pre.0.conv.weight")):
-            rows, idx, o = [], {}, 0
-            for name, shape, kind, live in tab:
-                if kind != "cw" or not live or not keep(shape[2], name):
-                    continue
-                s, n, _ = offs[name]
-                rows.append((s, o, shape[0], shape[1], shape[2] * shape[3]))
-                T = shape[2] * shape[3]
-                idx[name] = (o, (shape[0], T, shape[1]) if mode == 0 else (shape[1], T, shape[0]))
-                o += (n + 3) // 4 * 4
-            tbl = torch.tensor(rows, dtype=torch.int64).to(device)
-            self._wlay[mode] = (tbl, torch.empty(max(o, 4), device=device), idx)
+        # [Cout][T][Cin] for KS > 1) and per backward (dgrad [Cin][T][Cout]):
+        # tables per conv precision, see set_conv_precision / _build_weight_tables
+        self._device = device
+        self.set_conv_precision(None)
 
     # -- structure helpers ------------------------------------------------
     def _node_for(self, name):
@@ -225,14 +215,82 @@ class StackedHourglass(nn.Module):
         s, c = self._sidx[bn]
         return self.flat_stats[s:s + c], self.flat_stats[s + c:s + 2 * c]
 
+    def set_conv_precision(self, name):
+        """Conv arithmetic (kernels.CONV_PRECISIONS; None = $UBPL_CONV_PRECISION or the default):
+        'f32'    every conv on the exact-f32 MFMA (conv.hip);
+        '6xbf16' the 3x3 convs (forward and data gradient) on split-bf16 MFMA with
+                 3 bf16 pieces per operand over pre-split activations (conv_split.hip
+                 PSA path, error at the f32 path's level), the rest f32;
+        '3xbf16' every conv with 16-channel contraction groups on the 2-piece
+                 register-staged split kernel (faster, ~2^-16 operands: not parity-grade).
+        The stem (7x7, stride 2, 3 input channels) always runs in f32."""
+        self.conv_pieces = Kn.conv_precision_pieces(name)
+        self._build_weight_tables()
+
+    def _build_weight_tables(self):
+        """Split path (_wsp[mode]): the convs the precision puts there whose
+        contraction runs over 16-channel groups (Cin for the forward, Cout for
+        the data gradient); f32 path: _wlay[mode] = every conv that needs a
+        re-layout, _wlay[("rest", mode)] = those of them not on the split path."""
+        tab, offs, device = self._table, self._offs, self._device
+        stem = "pre.0.conv.weight"
+        pieces = self.conv_pieces
+        self._wsp = {}
+        for mode in (0, 1):
+            rows, idx, o = [], {}, 0
+            for name, shape, kind, live in tab:
+                if kind != "cw" or not live or name == stem or not pieces or shape[1 if mode == 0 else 0] % 16:
+                    continue
+                if pieces == 3 and shape[2] != 3:
+                    continue
+                s, n, _ = offs[name]
+                T = shape[2] * shape[3]
+                rows.append((s, o, shape[0], shape[1], T))
+                idx[name] = (o, (shape[0], T, shape[1]) if mode == 0 else (shape[1], T, shape[0]))
+                o += (n + 7) // 8 * 8
+            buf = torch.empty(max(pieces, 1) * max(o, 8), dtype=torch.int16, device=device)
+            self._wsp[mode] = [torch.tensor(rows, dtype=torch.int64).reshape(-1, 5).to(device), max(o, 8), idx, buf]
+        self._wlay = {}
+        for mode in (0, 1):
+            need = (lambda ks, nm: ks > 1) if mode == 0 else (lambda ks, nm: nm != stem)
+            for key, keep in ((mode, need), (("rest", mode), lambda ks, nm, m=mode, f=need:
+                                               f(ks, nm) and nm not in self._wsp[m][2])):
+                rows, idx, o = [], {}, 0
+                for name, shape, kind, live in tab:
+                    if kind != "cw" or not live or not keep(shape[2], name):
+                        continue
+                    s, n, _ = offs[name]
+                    rows.append((s, o, shape[0], shape[1], shape[2] * shape[3]))
+                    T = shape[2] * shape[3]
+                    idx[name] = (o, (shape[0], T, shape[1]) if mode == 0 else (shape[1], T, shape[0]))
+                    o += (n + 3) // 4 * 4
+                tbl = torch.tensor(rows, dtype=torch.int64).reshape(-1, 5).to(device)
+                self._wlay[key] = (tbl, torch.empty(max(o, 4), device=device), idx, mode)
+
     def relayout_weights(self, mode):
-        tbl, buf, _ = self._wlay[mode]
-        Kn.conv_weights_relayout(self.flat_params, buf, tbl, mode)
+        if self.conv_pieces:
+            tbl, plane, _, buf = self._wsp[mode]
+            Kn.conv_weights_split(self.flat_params, buf, plane, tbl, mode, self.conv_pieces)
+            tbl, buf, _, m = self._wlay[("rest", mode)]
+            if tbl.shape[0]:
+                Kn.conv_weights_relayout(self.flat_params, buf, tbl, m)
+            return
+        tbl, buf, _, m = self._wlay[mode]
+        Kn.conv_weights_relayout(self.flat_params, buf, tbl, m)
 
     def W(self, mode, name):
-        _, buf, idx = self._wlay[mode]
+        key = ("rest", mode) if self.conv_pieces else mode
+        _, buf, idx, _ = self._wlay[key]
         o, shp = idx[name]
         return buf[o:o + shp[0] * shp[1] * shp[2]].view(shp)
+
+    def SW(self, mode, name):
+        """Split-bf16 weights of a conv (None when it is not on the split path)."""
+        _, plane, idx, buf = self._wsp[mode]
+        if not self.conv_pieces or name not in idx:
+            return None
+        o, shp = idx[name]
+        return Kn.SplitWeights(buf, plane, o, shp, self.conv_pieces)
 
     def live_params(self):
         return self.flat_params[:self.n_live]
@@ -398,6 +456,12 @@ class _Exec:
         w = self.m.P(name + ".weight")
         b = self.m.P(name + ".bias")
         ps, ph = (None, None) if pro is None else pro
+        ws = self.m.SW(0, name + ".weight") if stride == 1 else None
+        if ws is not None:
+            if ws.npieces == 3:
+                xs = Kn.split_activation(x, 3, (ws.shape[1] == 9) * 1, ps, ph)
+                return Kn.conv2d_forward_psa(xs, ws, b, res=res, out=out)
+            return Kn.conv2d_forward_split(x, ws, b, ps, ph, res=res, out=out)
         wt = self.m.W(0, name + ".weight") if w.shape[2] > 1 else None
         return Kn.conv2d_forward(x, w, b, stride, ps, ph, res=res, out=out, w_tap=wt)
 
@@ -458,6 +522,12 @@ class _Exec:
                         accumulate=True)
 
     def dgrad(self, name, dy, res=None, out=None):
+        ws = self.m.SW(1, name + ".weight")
+        if ws is not None:
+            if ws.npieces == 3:
+                ys = Kn.split_activation(dy, 3, (ws.shape[1] == 9) * 1)
+                return Kn.conv2d_forward_psa(ys, ws, None, res=res, out=out)
+            return Kn.conv2d_forward_split(dy, ws, None, res=res, out=out)
         return Kn.conv2d_dgrad(dy, None, res=res, out=out, wt=self.m.W(1, name + ".weight"))
 
     def residual_bwd(self, p, dout):

@@ -295,6 +295,112 @@ def conv_weights_relayout(src, dst, table, mode):
     call("ubpl_conv_weights_relayout", _p(src), _p(dst), _p(table), int(table.shape[0]), int(mode), stream())
 
 
+# Conv arithmetic: "f32" = exact-f32 MFMA (v_mfma_f32_32x32x2_f32); "3xbf16" /
+# "6xbf16" = split-bf16 MFMA with 2 / 3 bf16 pieces per f32 operand (3 / 6
+# piece products, f32 accumulation).  Value = pieces (0 for f32).
+CONV_PRECISIONS = {"f32": 0, "3xbf16": 2, "6xbf16": 3}
+DEFAULT_CONV_PRECISION = "6xbf16"
+
+
+def conv_precision_name(name=None):
+    import os
+    return name or os.environ.get("UBPL_CONV_PRECISION", DEFAULT_CONV_PRECISION)
+
+
+def conv_precision_pieces(name=None):
+    """Pieces for a precision name (default: $UBPL_CONV_PRECISION or DEFAULT_CONV_PRECISION)."""
+    import os
+    name = name or os.environ.get("UBPL_CONV_PRECISION", DEFAULT_CONV_PRECISION)
+    if name not in CONV_PRECISIONS:
+        raise ValueError("conv precision %r not in %s" % (name, sorted(CONV_PRECISIONS)))
+    return CONV_PRECISIONS[name]
+
+
+class SplitWeights:
+    """One conv's weights as `npieces` bf16 planes (conv_split.hip): a view into
+    a shared buffer `buf` (int16, planes `plane` elements apart) at element
+    offset `off`; shape = (rows, KS*KS, cols) of the GEMM A operand."""
+
+    __slots__ = ("buf", "plane", "off", "shape", "npieces")
+
+    def __init__(self, buf, plane, off, shape, npieces):
+        self.buf, self.plane, self.off, self.shape, self.npieces = buf, plane, off, shape, npieces
+
+    def ptr(self):
+        return self.buf.data_ptr() + 2 * self.off
+
+
+def conv_weights_split(src, dst, plane, table, mode, npieces):
+    """Batched split re-layout (table as conv_weights_relayout, dst int16)."""
+    call("ubpl_conv_weights_split", _p(src), _p(dst), int(plane), _p(table), int(table.shape[0]), int(mode),
+         int(npieces), stream())
+
+
+def conv_weight_split(w, mode, npieces):
+    """Single conv: SplitWeights for the forward (mode 0) or data gradient (mode 1)."""
+    Cout, Cin, KS, _ = w.shape
+    n = w.numel()
+    plane = (n + 7) // 8 * 8
+    buf = torch.empty(npieces * plane, device=w.device, dtype=torch.int16)
+    tbl = torch.tensor([[0, 0, Cout, Cin, KS * KS]], dtype=torch.int64).to(w.device)
+    conv_weights_split(w.contiguous(), buf, plane, tbl, mode, npieces)
+    shape = (Cout, KS * KS, Cin) if mode == 0 else (Cin, KS * KS, Cout)
+    return SplitWeights(buf, plane, 0, shape, npieces)
+
+
+def conv2d_forward_split(x, ws, bias, pscale=None, pshift=None, res=None, out=None):
+    """Split-bf16 MFMA conv (stride 1, KS in {1, 3}, Cin % 16 == 0); ws: SplitWeights."""
+    B, Cin, H, W = x.shape
+    Cout, T, wc = ws.shape
+    KS = int(round(T ** 0.5))
+    if wc != Cin:
+        raise AssertionError("{} {}".format(Cin, wc))
+    Ho, Wo = conv_out_hw(H, W, KS, 1)
+    y = torch.empty((B, Cout, Ho, Wo), device=x.device, dtype=F32) if out is None else out
+    nws = _lib.lib().ubpl_conv2d_forward_split_workspace(B, Cin, Cout, KS, Ho, Wo, ws.npieces)
+    slab = torch.empty(int(nws), device=x.device, dtype=F32) if nws > 0 else None
+    call("ubpl_conv2d_forward_split", _p(x), B, Cin, H, W, ws.ptr(), int(ws.plane), _p(bias), Cout, KS, 1,
+         _p(pscale), _p(pshift), _p(res), _p(y), Ho, Wo, _p(slab), int(ws.npieces), stream())
+    return y
+
+
+class SplitAct:
+    """Pre-split activations (conv_split.hip PSA layout): `npieces` bf16 planes of
+    [B][C/16][H+2pad][W+2pad][16] in an int16 buffer, planes `plane` elements apart."""
+
+    __slots__ = ("buf", "plane", "B", "C", "H", "W", "pad", "npieces")
+
+    def __init__(self, buf, plane, B, C, H, W, pad, npieces):
+        self.buf, self.plane, self.B, self.C, self.H, self.W = buf, plane, B, C, H, W
+        self.pad, self.npieces = pad, npieces
+
+
+def split_activation(x, npieces, pad, pscale=None, pshift=None, out=None):
+    """x [B,C,H,W] f32 -> SplitAct of relu(x*pscale + pshift) (or x), zero border `pad`."""
+    B, C, H, W = x.shape
+    plane = B * C * (H + 2 * pad) * (W + 2 * pad)
+    if out is None:
+        out = torch.empty(npieces * plane, device=x.device, dtype=torch.int16)
+    call("ubpl_split_activation", _p(x), B, C, H, W, _p(pscale), _p(pshift), int(pad), int(npieces), _p(out),
+         int(plane), stream())
+    return SplitAct(out, plane, B, C, H, W, pad, npieces)
+
+
+def conv2d_forward_psa(xs, ws, bias, res=None, out=None):
+    """Stride-1 conv of pre-split activations xs (SplitAct) with SplitWeights ws."""
+    Cout, T, wc = ws.shape
+    KS = int(round(T ** 0.5))
+    if wc != xs.C or ws.npieces != xs.npieces:
+        raise AssertionError("{} {} / pieces {} {}".format(xs.C, wc, xs.npieces, ws.npieces))
+    B, H, W = xs.B, xs.H, xs.W
+    y = torch.empty((B, Cout, H, W), device=xs.buf.device, dtype=F32) if out is None else out
+    nws = _lib.lib().ubpl_conv2d_forward_psa_workspace(B, xs.C, Cout, KS, H, W, ws.npieces)
+    slab = torch.empty(int(nws), device=xs.buf.device, dtype=F32) if nws > 0 else None
+    call("ubpl_conv2d_forward_psa", _p(xs.buf), int(xs.plane), B, xs.C, H, W, int(xs.pad), ws.ptr(), int(ws.plane),
+         _p(bias), Cout, KS, _p(res), _p(y), _p(slab), int(ws.npieces), stream())
+    return y
+
+
 def conv2d_dgrad(dy, w, res=None, out=None, wt=None):
     """dx of a stride-1 conv = conv(dy, flip(w)^T); res/out allow accumulation."""
     if wt is None:
