@@ -220,13 +220,35 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
         }
     };
 
+    // Accumulators start at bias (+ residual): those loads overlap the operand
+    // prologue instead of trailing the main loop, and the epilogue only stores.
+    // An element is read and written by the same thread, so res may alias y.
+    const int li = lane & 31, lk = lane >> 5;
+    int64_t obase[TN];
+    bool nok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn + 32 * j + li;
+        nok[j] = n < N;
+        const int64_t nc = nok[j] ? n : N - 1;
+        const int b = (int)(nc / P);
+        const int p = (int)(nc - (int64_t)b * P);
+        obase[j] = (int64_t)b * Cout * P + p;
+    }
     floatx16 acc[TM][TN];
+    const bool seed = slab == nullptr;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            for (int r = 0; r < 16; ++r) {
+                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk, Cout - 1);
+                float v = 0.f;
+                if (seed && bias) v = bias[m];
+                if (seed && res) v += res[obase[j] + (int64_t)m * P];
+                acc[i][j][r] = v;
+            }
 
     if (PRO) __syncthreads();  // s_sc / s_sh ready
     const int nkt = (k_end - k_begin + BK - 1) / BK;
@@ -243,7 +265,6 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
         load_a(k_begin + BK);
         load_b(k_begin + BK);
     }
-    const int li = lane & 31, lk = lane >> 5;
     for (int t = 0; t < nkt; ++t) {
         const int cur = t & 1;
         __syncthreads();   // tile t visible; tile t-1's reads of buffer cur^1 done
@@ -286,31 +307,7 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
         }
         return;
     }
-    // ---- epilogue: + bias (+ residual), coalesced along n.  Two phases: res
-    // may alias y, so every residual load is issued before the first store
-    // (interleaved, each load would wait for the previous store).  An element
-    // is read and written by the same thread, so aliasing stays correct.
-    int64_t obase[TN];
-    bool nok[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int64_t n = n0 + wn + 32 * j + li;
-        nok[j] = n < N;
-        const int64_t nc = nok[j] ? n : N - 1;
-        const int b = (int)(nc / P);
-        const int p = (int)(nc - (int64_t)b * P);
-        obase[j] = (int64_t)b * Cout * P + p;
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk, Cout - 1);
-                if (bias) acc[i][j][r] += bias[m];
-                if (res) acc[i][j][r] += res[obase[j] + (int64_t)m * P];
-            }
+    // ---- epilogue: stores, coalesced along n (bias / residual are in acc)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         if (!nok[j]) continue;

@@ -408,18 +408,37 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
         }
     };
 
+    // accumulators start at bias (+ residual): see conv.hip conv_fwd_kernel
+    const int li = lane & 31, h = lane >> 5;
+    int64_t obase[TN];
+    bool nok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn + 32 * j + li;
+        nok[j] = n < N;
+        const int64_t nc = nok[j] ? n : N - 1;
+        const int b = (int)(nc / P);
+        const int p = (int)(nc - (int64_t)b * P);
+        obase[j] = (int64_t)b * Cout * P + p;
+    }
     floatx16 acc[TM][TN];
+    const bool seed = slab == nullptr;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            for (int r = 0; r < 16; ++r) {
+                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, Cout - 1);
+                float v = 0.f;
+                if (seed && bias) v = bias[m];
+                if (seed && res) v += res[obase[j] + (int64_t)m * P];
+                acc[i][j][r] = v;
+            }
 
     const int nkt = (k_end - k_begin) >> 4;
     if (nkt > 0) stage(0, k_begin);
     if (nkt > 1) stage(1, k_begin + 16);
-    const int li = lane & 31, h = lane >> 5;
     for (int t = 0; t < nkt; ++t) {
         // retire stage t (this wave's DMA), then the barrier: every wave's
         // stage t has landed and every wave is done reading stage t-1
@@ -484,27 +503,6 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
         }
         return;
     }
-    int64_t obase[TN];
-    bool nok[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int64_t n = n0 + wn + 32 * j + li;
-        nok[j] = n < N;
-        const int64_t nc = nok[j] ? n : N - 1;
-        const int b = (int)(nc / P);
-        const int p = (int)(nc - (int64_t)b * P);
-        obase[j] = (int64_t)b * Cout * P + p;
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, Cout - 1);
-                if (bias) acc[i][j][r] += bias[m];
-                if (res) acc[i][j][r] += res[obase[j] + (int64_t)m * P];
-            }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         if (!nok[j]) continue;
