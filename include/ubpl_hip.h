@@ -119,6 +119,14 @@ int ubpl_conv2d_forward(const float* x, int B, int Cin, int H, int W, const floa
                         int KS, int stride, const float* pscale, const float* pshift, const float* res, float* y,
                         int Ho, int Wo, float* slab, void* stream);
 int ubpl_conv_weight_tapmajor(const float* w, int Cout, int Cin, int KS, float* wt, void* stream);
+/* 1x1 stride-1 conv fed by LDS-DMA, k-major weights wk [Cin][Cout] (the
+ * data-gradient re-layout of the conv; for a data gradient, the reference
+ * weights themselves): same semantics as ubpl_conv2d_forward with KS = 1.
+ * Cout % 4 == 0, P % 4 == 0, x / wk 16-B aligned, Cin <= 256 with a prologue. */
+int64_t ubpl_conv1x1_kmajor_workspace(int B, int Cin, int Cout, int P);
+int ubpl_conv1x1_forward_kmajor(const float* x, int B, int Cin, int P, const float* wk, const float* bias, int Cout,
+                                const float* pscale, const float* pshift, const float* res, float* y, float* slab,
+                                void* stream);
 /* Weight gradient (+ bias gradient), reference weight layout. */
 int64_t ubpl_conv2d_wgrad_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo);
 int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, int H, int W, int Cout, int KS, int stride,

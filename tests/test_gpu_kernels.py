@@ -359,3 +359,35 @@ def test_conv_fwd_dgrad_wgrad_vs_torch(case):
         F.conv2d(inp_r, w, b, st, (KS - 1) // 2).backward(dy)
         dx = Kn.conv2d_dgrad(dy.to(DEV), wd)
         _close(dx, inp_r.grad, rtol=1e-4, atol=sc_(inp_r.grad))
+
+
+@pytest.mark.parametrize("case", [
+    (2, 256, 16, 128, True, False), (2, 128, 16, 256, True, True), (3, 64, 32, 128, False, False),
+    (2, 256, 4, 256, True, True), (2, 16, 8, 256, False, True), (2, 256, 8, 16, False, False)])
+def test_conv1x1_dma_vs_torch(case):
+    """LDS-DMA 1x1 kernel (k-major weights): forward with prologue / residual
+    (also aliasing the output) and the data gradient (weights as they lie)."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, H, Cout, pro, resid = case
+    gen = torch.Generator().manual_seed(31 + hash(case) % 1000)
+    x = torch.randn(B, Cin, H, H, generator=gen)
+    w = torch.randn(Cout, Cin, 1, 1, generator=gen) / np.sqrt(Cin)
+    b = torch.randn(Cout, generator=gen)
+    sc, sh = torch.rand(Cin, generator=gen) + 0.5, torch.randn(Cin, generator=gen) * 0.5
+    res = torch.randn(B, Cout, H, H, generator=gen)
+    inp = F.relu(x * sc[None, :, None, None] + sh[None, :, None, None]) if pro else x
+    yref = F.conv2d(inp, w, b) + (res if resid else 0)
+    d = lambda t: t.to(DEV)
+    wk = Kn.conv_weight_flip(d(w))
+    ps, ph = (d(sc), d(sh)) if pro else (None, None)
+    y = Kn.conv1x1_forward_kmajor(d(x), wk, d(b), ps, ph, res=d(res) if resid else None)
+    sc_ = lambda t: 1e-5 * float(t.abs().max())
+    _close(y, yref, rtol=1e-4, atol=sc_(yref))
+    if resid:
+        r2 = d(res)
+        y2 = Kn.conv1x1_forward_kmajor(d(x), wk, d(b), ps, ph, res=r2, out=r2)
+        _close(y2, yref, rtol=1e-4, atol=sc_(yref))
+    dy = torch.randn(B, Cout, H, H, generator=gen)
+    dxref = torch.nn.grad.conv2d_input(x.shape, w, dy)
+    dx = Kn.conv1x1_forward_kmajor(d(dy), d(w), None)
+    _close(dx, dxref, rtol=1e-4, atol=sc_(dxref))

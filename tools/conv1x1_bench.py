@@ -37,20 +37,32 @@ def main():
             ("pro+res", lambda: Kn.conv2d_forward(x, w, b, 1, ps, ph, res=res, out=y), mb(x, y, res)),
             ("pro+res=out", lambda: Kn.conv2d_forward(x, w, b, 1, ps, ph, res=res, out=res), mb(x, res, res)),
         ]
+        wk = Kn.conv_weight_flip(w)       # [Cin][1][Cout] = k-major
+        cases += [
+            ("dma plain", lambda: Kn.conv1x1_forward_kmajor(x, wk, b, out=y), mb(x, y)),
+            ("dma pro", lambda: Kn.conv1x1_forward_kmajor(x, wk, b, ps, ph, out=y), mb(x, y)),
+            ("dma pro+res", lambda: Kn.conv1x1_forward_kmajor(x, wk, b, ps, ph, res=res, out=y), mb(x, y, res)),
+        ]
+        yd = Kn.conv1x1_forward_kmajor(x, wk, b, ps, ph, res=res)
+        yr = Kn.conv2d_forward(x, w, b, 1, ps, ph, res=res)
+        print("dma vs f32 kernel rel %.2e" % float((yd - yr).norm() / yr.norm()))
         for name, fn, mbytes in cases:
             t = timeit(fn, reps)
             print("1x1 %3d->%3d %-12s %7.3f ms %6.1f TF %6.2f TB/s" % (cin, cout, name, t, fl / t / 1e9,
-                                                                     mbytes / t / 1e6))
+                                                                     mbytes / t / 1e3))
         dy = torch.randn(B, cout, H, H, device=dev, generator=g)
         wd = Kn.conv_weight_flip(w)
         dx = torch.empty_like(x)
         t = timeit(lambda: Kn.conv2d_dgrad(dy, None, out=dx, wt=wd), reps)
         print("1x1 %3d->%3d %-12s %7.3f ms %6.1f TF %6.2f TB/s" % (cin, cout, "dgrad", t, fl / t / 1e9,
-                                                                 mb(dy, dx) / t / 1e6))
+                                                                 mb(dy, dx) / t / 1e3))
+        t = timeit(lambda: Kn.conv1x1_forward_kmajor(dy, w, None, out=dx), reps)
+        print("1x1 %3d->%3d %-12s %7.3f ms %6.1f TF %6.2f TB/s" % (cin, cout, "dma dgrad", t, fl / t / 1e9,
+                                                                 mb(dy, dx) / t / 1e3))
         dw, db = torch.zeros_like(w), torch.zeros_like(b)
         t = timeit(lambda: Kn.conv2d_wgrad(dy, x, 1, 1, dw, db, ps, ph, accumulate=False), reps)
         print("1x1 %3d->%3d %-12s %7.3f ms %6.1f TF %6.2f TB/s" % (cin, cout, "wgrad", t, fl / t / 1e9,
-                                                                 mb(dy, x) / t / 1e6))
+                                                                 mb(dy, x) / t / 1e3))
 
 
 if __name__ == "__main__":

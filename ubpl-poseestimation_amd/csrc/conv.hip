@@ -235,8 +235,12 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
         const int p = (int)(nc - (int64_t)b * P);
         obase[j] = (int64_t)b * Cout * P + p;
     }
+    // (unconditional loads from always-valid pointers, then selects: a load
+    // under a runtime condition becomes a branch + vmcnt(0) per element)
     floatx16 acc[TM][TN];
-    const bool seed = slab == nullptr;
+    const bool hb = slab == nullptr && bias != nullptr, hr = slab == nullptr && res != nullptr;
+    const float* bp = bias ? bias : y;
+    const float* rp = res ? res : y;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -244,10 +248,8 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk, Cout - 1);
-                float v = 0.f;
-                if (seed && bias) v = bias[m];
-                if (seed && res) v += res[obase[j] + (int64_t)m * P];
-                acc[i][j][r] = v;
+                const float bv = bp[m], rv = rp[obase[j] + (int64_t)m * P];
+                acc[i][j][r] = (hb ? bv : 0.f) + (hr ? rv : 0.f);
             }
 
     if (PRO) __syncthreads();  // s_sc / s_sh ready
@@ -317,6 +319,194 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
                 if (m < Cout) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+            }
+    }
+}
+
+// ------------------------------------------------------------------ 1x1, LDS-DMA fed
+// 1x1 stride-1 conv as Y[m, n] = sum_k Wk[k][m] * X[b, k, p] (n = b*P + p)
+// with the weights k-major ([Cin][Cout]: the data-gradient re-layout of a 1x1
+// conv, or the reference layout itself for a data gradient).  Both operand
+// tiles are k-rows of contiguous floats — BN (128) pixels of one input channel
+// (NCHW as it lies) and BM output channels — so they go global -> LDS by
+// LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction), no staging
+// registers.  The fused pre-activation relu(x*scale + shift) is applied to the
+// B fragment after its LDS read (2 VALU per 2 MFMAs).  3-stage ring with
+// counted vmcnt and a raw s_barrier, as conv_split.hip's conv_psa_kernel.
+// Fragment reads are ds_read_b32 of 32 consecutive floats per half-wave
+// (conflict-free, no swizzle).
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, bool PRO>
+__global__ void __launch_bounds__(NT, 2) conv1x1_dma_kernel(const float* __restrict__ x, const float* __restrict__ wk,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ pscale,
+                                                          const float* __restrict__ pshift, const float* res,
+                                                          float* y, int B, int K, int P, int M, int kchunk,
+                                                          float* __restrict__ slab) {
+    constexpr int BN1 = 128;
+    constexpr int TM = BM / 64, TN = BN1 / 64;
+    constexpr int NS = 3;
+    constexpr int AB = BK * BM * 4, BB = BK * BN1 * 4;       // bytes per stage
+    constexpr int A_INS = AB / 1024, B_INS = BB / 1024;     // DMA instructions per stage
+    constexpr int A_PW = A_INS / 4, B_PW = B_INS / 4;       // per wave
+    constexpr int A_RPI = 1024 / (BM * 4);                  // rows per A instruction
+    __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
+
+    const int64_t N = (int64_t)B * P;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN1 / 2);
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                              gridDim.x * gridDim.y * gridDim.z);
+    const int by = lam % gridDim.y, bx = (lam / gridDim.y) % gridDim.x, bz = lam / (gridDim.y * gridDim.x);
+    const int m0 = by * BM;
+    const int64_t n0 = (int64_t)bx * BN1;
+    const int k_begin = bz * kchunk;
+    const int k_end = min(K, k_begin + kchunk);
+
+    // DMA sources (per lane, k-independent part).  A instruction q (of A_INS)
+    // covers k rows q*A_RPI .. +A_RPI-1; lane L: row q*A_RPI + L / (BM/4),
+    // columns 4*(L % (BM/4)) .. +3.  B instruction q: rows 2q, 2q+1; lane L:
+    // row 2q + (L >> 5), pixels 4*(L & 31) .. +3 of the tile.
+    const int a_row = lane / (BM / 4);
+    const int a_col = min(m0 + 4 * (lane % (BM / 4)), M - 4);
+    const int b_row = lane >> 5;
+    int64_t b_off;   // offset of (b, k=0, p) in x
+    {
+        int64_t n = n0 + 4 * (lane & 31);
+        n = n < N ? n : N - 4;
+        const int64_t b = n / P;
+        b_off = b * K * P + (n - b * P);
+    }
+    auto stage = [&](int buf, int kt) {
+        char* base = lds + buf * (AB + BB);
+#pragma unroll
+        for (int i = 0; i < A_PW; ++i) {
+            const int q = wid * A_PW + i;
+            const int k = min(kt + q * A_RPI + a_row, K - 1);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(wk + (int64_t)k * M + a_col), (lds_ptr_t)(base + q * 1024),
+                                             16, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < B_PW; ++i) {
+            const int q = wid * B_PW + i;
+            const int k = min(kt + 2 * q + b_row, K - 1);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(x + b_off + (int64_t)k * P),
+                                             (lds_ptr_t)(base + AB + q * 1024), 16, 0, 0);
+        }
+    };
+
+    // accumulators start at bias (+ residual), as conv_fwd_kernel
+    const int li = lane & 31, lk = lane >> 5;
+    int64_t obase[TN];
+    bool nok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn + 32 * j + li;
+        nok[j] = n < N;
+        const int64_t nc = nok[j] ? n : N - 1;
+        const int b = (int)(nc / P);
+        const int p = (int)(nc - (int64_t)b * P);
+        obase[j] = (int64_t)b * M * P + p;
+    }
+    // (unconditional loads from always-valid pointers, then selects: a load
+    // under a runtime condition becomes a branch + vmcnt(0) per element)
+    floatx16 acc[TM][TN];
+    const bool hb = slab == nullptr && bias != nullptr, hr = slab == nullptr && res != nullptr;
+    const float* bp = bias ? bias : y;
+    const float* rp = res ? res : y;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk, M - 1);
+                const float bv = bp[m], rv = rp[obase[j] + (int64_t)m * P];
+                acc[i][j][r] = (hb ? bv : 0.f) + (hr ? rv : 0.f);
+            }
+
+    const int nkt = (k_end - k_begin + BK - 1) / BK;
+    if (nkt > 0) stage(0, k_begin);
+    if (nkt > 1) stage(1, k_begin + BK);
+    for (int t = 0; t < nkt; ++t) {
+        if (t + 1 < nkt) vm_wait<A_PW + B_PW>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + 2 < nkt) stage((t + 2) % NS, k_begin + (t + 2) * BK);
+        const int kt = k_begin + t * BK;
+        const float* As = reinterpret_cast<const float*>(lds + (t % NS) * (AB + BB));
+        const float* Bs = reinterpret_cast<const float*>(lds + (t % NS) * (AB + BB) + AB);
+        // the K step's 16 (scale, shift) pairs by scalar loads (kt is uniform;
+        // an LDS table would alias the DMA images and cost a vmcnt(0) per step)
+        float scs[BK], shs[BK];
+        if (PRO) {
+            const int kb = __builtin_amdgcn_readfirstlane(min(kt, K - BK));
+#pragma unroll
+            for (int q = 0; q < BK; ++q) {
+                scs[q] = pscale[kb + q];
+                shs[q] = pshift[kb + q];
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < BK / 2; ++s) {
+            const int kr = 2 * s + lk;
+            const bool kok = kt + kr < k_end;        // K tail: zero the B fragment
+            float af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = As[kr * BM + wm + 32 * i + li];
+            float sc = 1.f, sh = 0.f;
+            if (PRO) {
+                sc = lk ? scs[2 * s + 1] : scs[2 * s];
+                sh = lk ? shs[2 * s + 1] : shs[2 * s];
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                float v = Bs[kr * BN1 + wn + 32 * j + li];
+                if (PRO) v = fmaxf(fmaf(v, sc, sh), 0.f);
+                bf[j] = kok ? v : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    if (slab != nullptr) {
+        float* sl = slab + (int64_t)bz * M * N;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int64_t n = n0 + wn + 32 * j + li;
+            if (n >= N) continue;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+                    if (m < M) sl[(int64_t)m * N + n] = acc[i][j][r];
+                }
+        }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        if (!nok[j]) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+                if (m < M) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
             }
     }
 }
@@ -834,6 +1024,7 @@ struct Plan {
 struct Device {
     int ncu = 256;
     int occ_fwd128 = 4, occ_fwd64 = 5, occ_wgrad = 4;
+    int occ_dma128 = 2, occ_dma64 = 2;
     int occ_w2[2][2] = {{8, 5}, {5, 4}};   // [bm == 128][bn == 128]
 };
 
@@ -866,7 +1057,7 @@ int best_split(int64_t tiles, int64_t nsteps, int maxs, int occ, int ncu, double
 }
 
 // Tile height + split-K for the forward (BN = 128, BK = 16).
-Plan fwd_plan(int Cout, int64_t N, int Ktot, int bn) {
+Plan fwd_plan(int Cout, int64_t N, int Ktot, int bn, bool dma = false) {
     const Device& d = device_info();
     const int nkt = (Ktot + BK - 1) / BK;
     const int maxs = nkt / 2 > 0 ? nkt / 2 : 1;            // >= 2 K steps per split
@@ -875,7 +1066,7 @@ Plan fwd_plan(int Cout, int64_t N, int Ktot, int bn) {
     for (int bm : {128, 64}) {
         if (bm == 128 && Cout <= 64) continue;
         const int64_t tiles = ((Cout + bm - 1) / bm) * ((N + bn - 1) / bn);
-        const int occ = bm == 128 ? d.occ_fwd128 : d.occ_fwd64;
+        const int occ = dma ? (bm == 128 ? d.occ_dma128 : d.occ_dma64) : (bm == 128 ? d.occ_fwd128 : d.occ_fwd64);
         const double sf = 2.0 * bm * bn * BK;
         const int s = best_split(tiles, nkt, maxs, occ, d.ncu, sf, 4.0 * Cout * N);
         // 64-row tiles re-read the B operand twice as often: ~15% slower per flop (measured)
@@ -1050,6 +1241,8 @@ const Device& device_info() {
             int v2 = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v2, f, NT, 0) == hipSuccess && v2 > 0) dst = v2;
         };
+        q((const void*)conv1x1_dma_kernel<128, true>, r.occ_dma128);
+        q((const void*)conv1x1_dma_kernel<64, true>, r.occ_dma64);
         q((const void*)conv_wgrad2_kernel<64, 64, 3, 1, true, false>, r.occ_w2[0][0]);
         q((const void*)conv_wgrad2_kernel<64, 128, 3, 1, true, false>, r.occ_w2[0][1]);
         q((const void*)conv_wgrad2_kernel<128, 64, 3, 1, true, false>, r.occ_w2[1][0]);
@@ -1061,6 +1254,54 @@ const Device& device_info() {
 }
 
 }  // namespace
+
+namespace {
+template <int BM, bool PRO>
+int launch_1x1_dma(const float* x, const float* wk, const float* bias, const float* ps, const float* sh,
+                   const float* res, float* y, int B, int K, int P, int M, const Plan& pl, float* slab,
+                   hipStream_t st) {
+    const int64_t N = (int64_t)B * P;
+    dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + BM - 1) / BM), (unsigned)pl.splits);
+    const bool split = pl.splits > 1;
+    hipLaunchKernelGGL((conv1x1_dma_kernel<BM, PRO>), grid, dim3(NT), 0, st, x, wk, bias, ps, sh,
+                       split ? nullptr : res, y, B, K, P, M, pl.kchunk, split ? slab : nullptr);
+    UBPL_LAUNCH_CHECK();
+    if (split) {
+        const int64_t total = (int64_t)M * N;
+        int g = (int)((total + 255) / 256);
+        if (g > 8192) g = 8192;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, slab, pl.splits, M, P, N, bias, res, y);
+        UBPL_LAUNCH_CHECK();
+    }
+    return 0;
+}
+}  // namespace
+
+UBPL_API int64_t ubpl_conv1x1_kmajor_workspace(int B, int Cin, int Cout, int P) {
+    const Plan pl = fwd_plan(Cout, (int64_t)B * P, Cin, 128, true);
+    return pl.splits > 1 ? (int64_t)pl.splits * Cout * B * P : 0;
+}
+
+// 1x1 stride-1 conv with k-major weights wk [Cin][Cout] (the data-gradient
+// re-layout of a 1x1 conv; for a data gradient, the reference weights
+// themselves): y[B,Cout,P] = conv(relu(x*pscale + pshift) or x) + bias (+ res,
+// may alias y).  Needs Cout % 4 == 0, P % 4 == 0, Cin <= 256 with a prologue,
+// 16-B aligned x / wk.  slab: ubpl_conv1x1_kmajor_workspace floats (nullable at 0).
+UBPL_API int ubpl_conv1x1_forward_kmajor(const float* x, int B, int Cin, int P, const float* wk, const float* bias,
+                                         int Cout, const float* pscale, const float* pshift, const float* res,
+                                         float* y, float* slab, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const bool pro = pscale != nullptr;
+    if ((pro && Cin > MAXC) || Cout % 4 != 0 || P % 4 != 0 || (((uintptr_t)x) & 15) || (((uintptr_t)wk) & 15))
+        return (int)hipErrorInvalidValue;
+    const Plan pl = fwd_plan(Cout, (int64_t)B * P, Cin, 128, true);
+    if (pl.splits > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
+    if (pl.bm == 128)
+        return pro ? launch_1x1_dma<128, true>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, st)
+                   : launch_1x1_dma<128, false>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, st);
+    return pro ? launch_1x1_dma<64, true>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, st)
+               : launch_1x1_dma<64, false>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, st);
+}
 
 // Floats of workspace ubpl_conv2d_forward needs (split-K slab); 0 = none.
 // w must be in the layout of ubpl_conv_weight_tapmajor for KS > 1.

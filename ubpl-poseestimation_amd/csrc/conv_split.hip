@@ -421,8 +421,12 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
         const int p = (int)(nc - (int64_t)b * P);
         obase[j] = (int64_t)b * Cout * P + p;
     }
+    // (unconditional loads from always-valid pointers, then selects: a load
+    // under a runtime condition becomes a branch + vmcnt(0) per element)
     floatx16 acc[TM][TN];
-    const bool seed = slab == nullptr;
+    const bool hb = slab == nullptr && bias != nullptr, hr = slab == nullptr && res != nullptr;
+    const float* bp = bias ? bias : y;
+    const float* rp = res ? res : y;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -430,10 +434,8 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, Cout - 1);
-                float v = 0.f;
-                if (seed && bias) v = bias[m];
-                if (seed && res) v += res[obase[j] + (int64_t)m * P];
-                acc[i][j][r] = v;
+                const float bv = bp[m], rv = rp[obase[j] + (int64_t)m * P];
+                acc[i][j][r] = (hb ? bv : 0.f) + (hr ? rv : 0.f);
             }
 
     const int nkt = (k_end - k_begin) >> 4;

@@ -36,6 +36,8 @@ SIGNATURES = {
     "ubpl_bn_backward": (I, [P, P, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, P, P]),
     "ubpl_conv2d_forward": (I, [P, I, I, I, I, P, P, I, I, I, P, P, P, P, I, I, P, P]),
     "ubpl_conv2d_forward_workspace": (L, [I, I, I, I, I, I]),
+    "ubpl_conv1x1_kmajor_workspace": (L, [I, I, I, I]),
+    "ubpl_conv1x1_forward_kmajor": (I, [P, I, I, I, P, P, I, P, P, P, P, P, P]),
     "ubpl_conv_weight_tapmajor": (I, [P, I, I, I, P, P]),
     "ubpl_conv2d_wgrad_workspace": (L, [I, I, I, I, I, I]),
     "ubpl_conv2d_wgrad": (I, [P, P, I, I, I, I, I, I, I, P, P, I, I, P, P, P, I, P]),

@@ -351,6 +351,7 @@ class StackedHourglass(nn.Module):
         part = self._scratch(B, 64)
         ex = _Exec(self, B, dev, part, train=self.training, save=save)
         self.relayout_weights(0)
+        self.relayout_weights(1)       # k-major 1x1 weights for conv1x1_forward_kmajor
         if self.training:
             self._nbt.add_(1)
         else:
@@ -462,6 +463,8 @@ class _Exec:
                 xs = Kn.split_activation(x, 3, (ws.shape[1] == 9) * 1, ps, ph)
                 return Kn.conv2d_forward_psa(xs, ws, b, res=res, out=out)
             return Kn.conv2d_forward_split(x, ws, b, ps, ph, res=res, out=out)
+        if w.shape[2] == 1 and stride == 1 and Kn.conv1x1_kmajor_ok(x, w.shape[0]):
+            return Kn.conv1x1_forward_kmajor(x, self.m.W(1, name + ".weight"), b, ps, ph, res=res, out=out)
         wt = self.m.W(0, name + ".weight") if w.shape[2] > 1 else None
         return Kn.conv2d_forward(x, w, b, stride, ps, ph, res=res, out=out, w_tap=wt)
 
@@ -528,6 +531,9 @@ class _Exec:
                 ys = Kn.split_activation(dy, 3, (ws.shape[1] == 9) * 1)
                 return Kn.conv2d_forward_psa(ys, ws, None, res=res, out=out)
             return Kn.conv2d_forward_split(dy, ws, None, res=res, out=out)
+        w = self.m.P(name + ".weight")
+        if w.shape[2] == 1 and Kn.conv1x1_kmajor_ok(dy, w.shape[1]):
+            return Kn.conv1x1_forward_kmajor(dy, w, None, res=res, out=out)     # [Cout][Cin] = k-major
         return Kn.conv2d_dgrad(dy, None, res=res, out=out, wt=self.m.W(1, name + ".weight"))
 
     def residual_bwd(self, p, dout):

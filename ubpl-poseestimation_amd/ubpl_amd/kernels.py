@@ -273,6 +273,24 @@ def conv2d_forward(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out
     return y
 
 
+def conv1x1_kmajor_ok(x, cout):
+    """Shapes / alignment the LDS-DMA 1x1 kernel takes."""
+    return cout % 4 == 0 and (x.shape[2] * x.shape[3]) % 4 == 0 and x.data_ptr() % 16 == 0
+
+
+def conv1x1_forward_kmajor(x, wk, bias, pscale=None, pshift=None, res=None, out=None):
+    """1x1 stride-1 conv with k-major weights wk (Cin*Cout floats, [Cin][Cout]):
+    y = conv(relu(x*pscale + pshift) or x) + bias (+ res; res may alias out)."""
+    B, Cin, H, W = x.shape
+    Cout = wk.numel() // Cin
+    y = torch.empty((B, Cout, H, W), device=x.device, dtype=F32) if out is None else out
+    nws = _lib.lib().ubpl_conv1x1_kmajor_workspace(B, Cin, Cout, H * W)
+    slab = torch.empty(int(nws), device=x.device, dtype=F32) if nws > 0 else None
+    call("ubpl_conv1x1_forward_kmajor", _p(x), B, Cin, H * W, _p(wk), _p(bias), Cout, _p(pscale), _p(pshift),
+         _p(res), _p(y), _p(slab), stream())
+    return y
+
+
 def conv2d_wgrad(dy, x, KS, stride, dw, db, pscale=None, pshift=None, accumulate=True):
     B, Cin, H, W = x.shape
     Cout, Ho, Wo = dy.shape[1], dy.shape[2], dy.shape[3]
