@@ -30,6 +30,7 @@
 // 32 consecutive floats per half-wave; register-staged double buffer with one
 // barrier per K step.
 #include "common.h"
+#include <cstdlib>
 using ubpl::conv_kgroup;
 using ubpl::xcd_remap;
 
@@ -1059,12 +1060,18 @@ int best_split(int64_t tiles, int64_t nsteps, int maxs, int occ, int ncu, double
 // Tile height + split-K for the forward (BN = 128, BK = 16).
 Plan fwd_plan(int Cout, int64_t N, int Ktot, int bn, bool dma = false) {
     const Device& d = device_info();
+    // tuning hook: UBPL_DMA_BM=64|128 pins the 1x1 DMA kernel's tile height
+    static const int force_bm = [] {
+        const char* e = getenv("UBPL_DMA_BM");
+        return e ? atoi(e) : 0;
+    }();
     const int nkt = (Ktot + BK - 1) / BK;
     const int maxs = nkt / 2 > 0 ? nkt / 2 : 1;            // >= 2 K steps per split
     Plan best{64, 1, 0};
     double bc = 1e30;
     for (int bm : {128, 64}) {
         if (bm == 128 && Cout <= 64) continue;
+        if (dma && force_bm && bm != force_bm && !(force_bm == 128 && Cout <= 64)) continue;
         const int64_t tiles = ((Cout + bm - 1) / bm) * ((N + bn - 1) / bn);
         const int occ = dma ? (bm == 128 ? d.occ_dma128 : d.occ_dma64) : (bm == 128 ? d.occ_fwd128 : d.occ_fwd64);
         const double sf = 2.0 * bm * bn * BK;
