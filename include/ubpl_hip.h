@@ -100,6 +100,16 @@ int ubpl_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmea
                         int C, float* scale, float* shift, void* stream);
 int ubpl_bn_apply(const float* x, int B, int C, int HW, const float* scale, const float* shift, int relu, float* y,
                   void* stream);
+/* Statistics from 64-pixel partials: part [C][ceil(N/64)][2] f32 = (S, M2) =
+ * (sum y, sum (y - S/n)^2) over each 64-pixel slice of the flat (b, p) pixels of
+ * y [B,C,P] (Chan's parallel form); the conv kernels write it from their
+ * accumulators (stat_part arguments), ubpl_bn_partials from a tensor.
+ * ubpl_bn_stats_from_partials: outputs as ubpl_bn_forward_stats, f64 combine. */
+int64_t ubpl_bn_partial_floats(int C, int64_t N);
+int ubpl_bn_partials(const float* y, int B, int C, int P, float* part, void* stream);
+int ubpl_bn_stats_from_partials(const float* part, int C, int64_t N, const float* gamma,
+                                const float* beta, float eps, float momentum, float* rmean, float* rvar,
+                                float* mean_out, float* invstd_out, float* scale, float* shift_out, void* stream);
 /* Backward of y = [relu](bn(x)); dgamma/dbeta accumulate; dx = add1 + add2 + dL/dx. */
 int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma, const float* mean,
                      const float* invstd, const float* scale, const float* shift, int relu, double* part,
@@ -126,7 +136,7 @@ int ubpl_conv_weight_tapmajor(const float* w, int Cout, int Cin, int KS, float* 
 int64_t ubpl_conv1x1_kmajor_workspace(int B, int Cin, int Cout, int P);
 int ubpl_conv1x1_forward_kmajor(const float* x, int B, int Cin, int P, const float* wk, const float* bias, int Cout,
                                 const float* pscale, const float* pshift, const float* res, float* y, float* slab,
-                                void* stream);
+                                float* stat_part, void* stream);
 /* Weight gradient (+ bias gradient), reference weight layout. */
 int64_t ubpl_conv2d_wgrad_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo);
 int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, int H, int W, int Cout, int KS, int stride,
@@ -165,7 +175,7 @@ int ubpl_split_activation(const float* x, int B, int C, int H, int W, const floa
 int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int KS, int H, int W, int npieces);
 int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                             const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
-                            const float* res, float* y, float* slab, int npieces, void* stream);
+                            const float* res, float* y, float* slab, int npieces, float* stat_part, void* stream);
 
 /* MaxPool2d(2,2) (models/base/layers.py:93), Upsample(x2, nearest) + add
  * (layers.py:110-111), AvgPool2d(2,2) projection (models/pose/hourglass.py:226). */

@@ -391,3 +391,32 @@ def test_conv1x1_dma_vs_torch(case):
     dxref = torch.nn.grad.conv2d_input(x.shape, w, dy)
     dx = Kn.conv1x1_forward_kmajor(d(dy), d(w), None)
     _close(dx, dxref, rtol=1e-4, atol=sc_(dxref))
+
+
+@pytest.mark.parametrize("case", [(4, 128, 32, 128, 1), (32, 256, 4, 128, 1), (2, 128, 64, 128, 3),
+                                  (4, 128, 8, 128, 3)])
+def test_conv_epilogue_bn_partials(case):
+    """BatchNorm statistics from the partials the conv epilogue writes (and the
+    split-K fallback pass) equal the statistics of the conv output."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, H, Cout, KS = case
+    gen = torch.Generator().manual_seed(7 + hash(case) % 1000)
+    x = torch.randn(B, Cin, H, H, generator=gen).to(DEV)
+    w = (torch.randn(Cout, Cin, KS, KS, generator=gen) / np.sqrt(Cin * KS * KS)).to(DEV)
+    b = (torch.randn(Cout, generator=gen) * 3).to(DEV)
+    gamma, beta = torch.rand(Cout, device=DEV) + 0.5, torch.randn(Cout, device=DEV)
+    part = Kn.bn_partial_buffer(Cout, B * H * H, DEV)
+    if KS == 1:
+        y = Kn.conv1x1_forward_kmajor(x, Kn.conv_weight_flip(w), b, stat_part=part)
+    else:
+        xs = Kn.split_activation(x, 3, 1)
+        y = Kn.conv2d_forward_psa(xs, Kn.conv_weight_split(w, 0, 3), b, stat_part=part)
+    rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    mu, istd, sc, sh = (torch.empty(Cout, device=DEV) for _ in range(4))
+    Kn.bn_stats_from_partials(part, Cout, B * H * H, gamma, beta, 1e-5, 0.1, rm, rv, mu, istd, sc, sh)
+    yd = y.double().cpu()
+    m_ref = yd.mean((0, 2, 3))
+    v_ref = yd.var((0, 2, 3), unbiased=False)
+    _close(mu, m_ref, rtol=1e-6, atol=1e-6)
+    _close(istd, 1.0 / torch.sqrt(v_ref + 1e-5), rtol=1e-5, atol=0)
+    _close(rv, 0.9 + 0.1 * yd.var((0, 2, 3), unbiased=True), rtol=1e-5, atol=0)

@@ -301,7 +301,92 @@ int grid_ew(int64_t n) {
 // partial sums.
 constexpr int MAXBN = 512;
 constexpr int CNT_DOUBLES = MAXBN / 2;
+// ---- statistics from 64-pixel partials (conv-epilogue fused: common.h
+// tile_bn_partials; or bn_partials_kernel below).  part [C][np][2] f32 =
+// (S, M2) per slice, Chan's parallel form.
+__global__ void __launch_bounds__(256) bn_partials_kernel(const float* __restrict__ y, int C, int P, int64_t N,
+                                                         float* __restrict__ part) {
+    const int64_t np = (N + 63) / 64;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (c, q)
+    if (i >= (int64_t)C * np) return;
+    const int c = (int)(i / np);
+    const int64_t q = i - (int64_t)c * np;
+    const int64_t n1 = min(N, q * 64 + 64);
+    float s = 0.f;
+    for (int64_t n = q * 64; n < n1; ++n) {
+        const int64_t b = n / P;
+        s += y[(b * C + c) * P + (n - b * P)];
+    }
+    const float mu = s / (float)(n1 - q * 64);
+    float m2 = 0.f;
+    for (int64_t n = q * 64; n < n1; ++n) {
+        const int64_t b = n / P;
+        const float d = y[(b * C + c) * P + (n - b * P)] - mu;
+        m2 = fmaf(d, d, m2);
+    }
+    part[i * 2] = s;
+    part[i * 2 + 1] = m2;
+}
+
+// mean = sum S / N; M2 = sum M2_q + sum n_q (S_q/n_q - mean)^2, in f64.
+__global__ void __launch_bounds__(256) bn_finalize_partials_kernel(const float* __restrict__ part, int64_t np,
+                                                                  int64_t N, StatsOut o) {
+    __shared__ double red[16];
+    const int c = blockIdx.x;
+    const float* pc = part + (int64_t)c * np * 2;
+    double t1 = 0.0;
+    for (int64_t q = threadIdx.x; q < np; q += blockDim.x) t1 += (double)pc[q * 2];
+    t1 = ubpl::block_sum(t1, red);
+    const double mean = t1 / (double)N;
+    double t2 = 0.0;
+    for (int64_t q = threadIdx.x; q < np; q += blockDim.x) {
+        const double nq = (double)(N - q * 64 < 64 ? N - q * 64 : 64);
+        const double dm = (double)pc[q * 2] / nq - mean;
+        t2 += (double)pc[q * 2 + 1] + nq * dm * dm;
+    }
+    t2 = ubpl::block_sum(t2, red);
+    if (threadIdx.x != 0) return;
+    const double var = t2 / (double)N;
+    const float invstd = (float)(1.0 / sqrt(var + (double)o.eps));
+    const float sc = invstd * o.gamma[c];
+    o.mean_out[c] = (float)mean;
+    o.invstd_out[c] = invstd;
+    o.scale[c] = sc;
+    o.shift[c] = o.beta[c] - (float)mean * sc;
+    if (o.rmean) {
+        const double unb = N > 1 ? var * (double)N / (double)(N - 1) : var;
+        o.rmean[c] = (float)((double)o.momentum * mean + (1.0 - (double)o.momentum) * (double)o.rmean[c]);
+        o.rvar[c] = (float)((double)o.momentum * unb + (1.0 - (double)o.momentum) * (double)o.rvar[c]);
+    }
+}
+
 UBPL_API int ubpl_bn_splits(int B, int C) { return splits_for(B, C); }
+
+// Floats of a partial-statistics buffer for C channels over N = B*P pixels.
+UBPL_API int64_t ubpl_bn_partial_floats(int C, int64_t N) { return 2 * (int64_t)C * ((N + 63) / 64); }
+
+// part [C][ceil(N/64)][2] = per 64-pixel slice (S, M2) of y [B,C,P]: the layout
+// conv epilogues produce themselves.
+UBPL_API int ubpl_bn_partials(const float* y, int B, int C, int P, float* part, void* stream) {
+    const int64_t N = (int64_t)B * P;
+    const int64_t n = (int64_t)C * ((N + 63) / 64);
+    hipLaunchKernelGGL(bn_partials_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, y, C,
+                       P, N, part);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// Train-mode BatchNorm statistics from partials (outputs as ubpl_bn_forward_stats).
+UBPL_API int ubpl_bn_stats_from_partials(const float* part, int C, int64_t N, const float* gamma,
+                                         const float* beta, float eps, float momentum, float* rmean, float* rvar,
+                                         float* mean_out, float* invstd_out, float* scale, float* shift_out,
+                                         void* stream) {
+    StatsOut o{gamma, beta, eps, momentum, rmean, rvar, mean_out, invstd_out, scale, shift_out};
+    hipLaunchKernelGGL(bn_finalize_partials_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part,
+                       (N + 63) / 64, N, o);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
 UBPL_API int64_t ubpl_bn_part_doubles(int B, int C) { return CNT_DOUBLES + 2 * (int64_t)C * splits_for(B, C); }
 
 // Train-mode statistics of x [B,C,H,W] -> mean, invstd, (scale, shift) and the

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ubpl_hip.h"
+
 #define UBPL_API extern "C" __attribute__((visibility("default")))
 
 #define UBPL_LAUNCH_CHECK()                         \
@@ -77,5 +79,59 @@ __device__ __forceinline__ float block_max(float v, float* smem) {
 }
 
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// Sum over the 32 lanes of each wave half by DPP row shifts (Hillis-Steele
+// within a 16-lane row, then row_bcast:15 into rows 1 and 3): the total of
+// lanes 0-31 lands in lane 31, of lanes 32-63 in lane 63.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
+                                                                     true));
+}
+__device__ __forceinline__ float half_sum_dpp(float v) {
+    v = dpp_add<0x111>(v);   // row_shr:1
+    v = dpp_add<0x112>(v);   // row_shr:2
+    v = dpp_add<0x114>(v);   // row_shr:4
+    v = dpp_add<0x118>(v);   // row_shr:8
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xA, 0xF,
+                                                                     false));   // row_bcast:15
+}
+
+// BatchNorm partial statistics of a conv output tile, straight from the MFMA
+// accumulators (C/D map: lane l holds pixel n0 + l&31 of rows (r&3) + 8(r>>2) +
+// 4(l>>5)): per channel m and per 64-pixel slice q = n/64 of the flat (b, p)
+// range, part[(m*np + q)*2 + {0,1}] = (S, M2): S = sum y, M2 = sum (y - S/n)^2
+// over the slice's n valid pixels (Chan's parallel form: no E[y^2] - E[y]^2
+// cancellation; the finalize combines slices in f64).  A wave covers one slice
+// (its 64 pixels: TN = 2 fragments of 32).
+template <int TM, int TN, typename ACC>
+__device__ __forceinline__ void tile_bn_partials(const ACC (&acc)[TM][TN], const bool (&nok)[TN], int mrow0, int M,
+                                                 int64_t nwave0, int64_t N, float* part) {
+    static_assert(TN == 2, "one wave = one 64-pixel slice");
+    if (nwave0 >= N) return;
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int64_t np = (N + 63) / 64;
+    const int64_t q = nwave0 / 64;
+    const float inv_n = 1.f / (float)(N - nwave0 < 64 ? N - nwave0 : 64);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float y0 = nok[0] ? acc[i][0][r] : 0.f;
+            const float y1 = nok[1] ? acc[i][1][r] : 0.f;
+            const float s = half_sum_dpp(y0 + y1);
+            const float s_lo = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s), 31));
+            const float s_hi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s), 63));
+            const float mu = (h ? s_hi : s_lo) * inv_n;
+            const float d0 = nok[0] ? y0 - mu : 0.f;
+            const float d1 = nok[1] ? y1 - mu : 0.f;
+            const float m2 = half_sum_dpp(fmaf(d0, d0, d1 * d1));
+            if ((lane & 31) == 31 && m < M) {
+                part[(m * np + q) * 2] = s;
+                part[(m * np + q) * 2 + 1] = m2;
+            }
+        }
+}
 
 }  // namespace ubpl

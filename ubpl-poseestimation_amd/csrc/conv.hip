@@ -350,7 +350,7 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_dma_kernel(const float* __restr
                                                           const float* __restrict__ pscale,
                                                           const float* __restrict__ pshift, const float* res,
                                                           float* y, int B, int K, int P, int M, int kchunk,
-                                                          float* __restrict__ slab) {
+                                                          float* __restrict__ slab, float* __restrict__ stat_part) {
     constexpr int BN1 = 128;
     constexpr int TM = BM / 64, TN = BN1 / 64;
     constexpr int NS = 3;
@@ -499,6 +499,7 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_dma_kernel(const float* __restr
         }
         return;
     }
+    if (stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0 + wm, M, n0 + wn, N, stat_part);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         if (!nok[j]) continue;
@@ -1266,12 +1267,13 @@ namespace {
 template <int BM, bool PRO>
 int launch_1x1_dma(const float* x, const float* wk, const float* bias, const float* ps, const float* sh,
                    const float* res, float* y, int B, int K, int P, int M, const Plan& pl, float* slab,
-                   hipStream_t st) {
+                   float* stat_part, hipStream_t st) {
     const int64_t N = (int64_t)B * P;
     dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + BM - 1) / BM), (unsigned)pl.splits);
     const bool split = pl.splits > 1;
     hipLaunchKernelGGL((conv1x1_dma_kernel<BM, PRO>), grid, dim3(NT), 0, st, x, wk, bias, ps, sh,
-                       split ? nullptr : res, y, B, K, P, M, pl.kchunk, split ? slab : nullptr);
+                       split ? nullptr : res, y, B, K, P, M, pl.kchunk, split ? slab : nullptr,
+                       split ? nullptr : stat_part);
     UBPL_LAUNCH_CHECK();
     if (split) {
         const int64_t total = (int64_t)M * N;
@@ -1279,6 +1281,7 @@ int launch_1x1_dma(const float* x, const float* wk, const float* bias, const flo
         if (g > 8192) g = 8192;
         hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, st, slab, pl.splits, M, P, N, bias, res, y);
         UBPL_LAUNCH_CHECK();
+        if (stat_part) return ubpl_bn_partials(y, B, M, P, stat_part, st);
     }
     return 0;
 }
@@ -1294,9 +1297,10 @@ UBPL_API int64_t ubpl_conv1x1_kmajor_workspace(int B, int Cin, int Cout, int P) 
 // themselves): y[B,Cout,P] = conv(relu(x*pscale + pshift) or x) + bias (+ res,
 // may alias y).  Needs Cout % 4 == 0, P % 4 == 0, Cin <= 256 with a prologue,
 // 16-B aligned x / wk.  slab: ubpl_conv1x1_kmajor_workspace floats (nullable at 0).
+// stat_part (nullable): BatchNorm partials of y (ubpl_bn_partials layout).
 UBPL_API int ubpl_conv1x1_forward_kmajor(const float* x, int B, int Cin, int P, const float* wk, const float* bias,
                                          int Cout, const float* pscale, const float* pshift, const float* res,
-                                         float* y, float* slab, void* stream) {
+                                         float* y, float* slab, float* stat_part, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const bool pro = pscale != nullptr;
     if ((pro && Cin > MAXC) || Cout % 4 != 0 || P % 4 != 0 || (((uintptr_t)x) & 15) || (((uintptr_t)wk) & 15))
@@ -1304,10 +1308,10 @@ UBPL_API int ubpl_conv1x1_forward_kmajor(const float* x, int B, int Cin, int P, 
     const Plan pl = fwd_plan(Cout, (int64_t)B * P, Cin, 128, true);
     if (pl.splits > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
     if (pl.bm == 128)
-        return pro ? launch_1x1_dma<128, true>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, st)
-                   : launch_1x1_dma<128, false>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, st);
-    return pro ? launch_1x1_dma<64, true>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, st)
-               : launch_1x1_dma<64, false>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, st);
+        return pro ? launch_1x1_dma<128, true>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, stat_part, st)
+                   : launch_1x1_dma<128, false>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, stat_part, st);
+    return pro ? launch_1x1_dma<64, true>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, stat_part, st)
+               : launch_1x1_dma<64, false>(x, wk, bias, pscale, pshift, res, y, B, Cin, P, Cout, pl, slab, stat_part, st);
 }
 
 // Floats of workspace ubpl_conv2d_forward needs (split-K slab); 0 = none.

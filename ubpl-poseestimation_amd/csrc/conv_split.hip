@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
                                                         int B, int Cin, int H, int W, int pad, int Cout, int kchunk,
-                                                        float* __restrict__ slab) {
+                                                        float* __restrict__ slab, float* __restrict__ stat_part) {
     constexpr int PADK = (KS - 1) / 2;
     constexpr int T = KS * KS;
     constexpr int TM = BM / 64, TN = BN / 64;
@@ -505,6 +505,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
         }
         return;
     }
+    if (stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0 + wm, Cout, n0 + wn, N, stat_part);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         if (!nok[j]) continue;
@@ -649,16 +650,18 @@ void launch_split_reduce(const float* slab, int splits, int Cout, int P, int64_t
 template <int BM, int KS, int NP>
 int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t wplane, const float* bias,
                const float* res, float* y, int B, int Cin, int H, int W, int pad, int Cout, const Plan& pl,
-               float* slab, hipStream_t st) {
+               float* slab, float* stat_part, hipStream_t st) {
     const int64_t N = (int64_t)B * H * W;
     dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
     const bool split = pl.splits > 1;
     hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP>), grid, dim3(NT), 0, st, xs, xplane, wp, wplane, bias,
-                       split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr);
+                       split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr,
+                       split ? nullptr : stat_part);
     UBPL_LAUNCH_CHECK();
     if (split) {
         launch_split_reduce(slab, pl.splits, Cout, H * W, N, bias, res, y, st);
         UBPL_LAUNCH_CHECK();
+        if (stat_part) return ubpl_bn_partials(y, B, Cout, H * W, stat_part, st);
     }
     return 0;
 }
@@ -817,7 +820,8 @@ UBPL_API int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int
 // npieces).  KS in {1, 3}; Cin % 16 == 0; res may alias y.
 UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                                      const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
-                                     const float* res, float* y, float* slab, int npieces, void* stream) {
+                                     const float* res, float* y, float* slab, int npieces, float* stat_part,
+                                     void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (Cin % 16 != 0 || (npieces != 2 && npieces != 3) || pad < (KS - 1) / 2) return (int)hipErrorInvalidValue;
     if ((((uintptr_t)wsplit) & 15) != 0 || (((uintptr_t)xs) & 15) != 0 || (wplane % 8) != 0 || (xplane % 8) != 0)
@@ -826,7 +830,8 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     const Plan pl = fwd_plan(Cout, N, Cin * KS * KS, npieces, true);
     if (pl.splits > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
 #define UBPL_PS(BM_, KS_, NP_) \
-    return launch_psa<BM_, KS_, NP_>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl, slab, st)
+    return launch_psa<BM_, KS_, NP_>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl, slab, \
+                                     stat_part, st)
 #define UBPL_PS_BM(KS_, NP_)          \
     if (pl.bm == 128) UBPL_PS(128, KS_, NP_); \
     UBPL_PS(64, KS_, NP_)

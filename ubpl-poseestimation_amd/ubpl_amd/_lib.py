@@ -33,11 +33,14 @@ SIGNATURES = {
     "ubpl_bn_forward_stats": (I, [P, I, I, I, P, P, F, F, P, P, P, P, P, P, P, P]),
     "ubpl_bn_eval_coeffs": (I, [P, P, P, P, F, I, P, P, P]),
     "ubpl_bn_apply": (I, [P, I, I, I, P, P, I, P, P]),
+    "ubpl_bn_partial_floats": (L, [I, L]),
+    "ubpl_bn_partials": (I, [P, I, I, I, P, P]),
+    "ubpl_bn_stats_from_partials": (I, [P, I, L, P, P, F, F, P, P, P, P, P, P, P]),
     "ubpl_bn_backward": (I, [P, P, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, P, P]),
     "ubpl_conv2d_forward": (I, [P, I, I, I, I, P, P, I, I, I, P, P, P, P, I, I, P, P]),
     "ubpl_conv2d_forward_workspace": (L, [I, I, I, I, I, I]),
     "ubpl_conv1x1_kmajor_workspace": (L, [I, I, I, I]),
-    "ubpl_conv1x1_forward_kmajor": (I, [P, I, I, I, P, P, I, P, P, P, P, P, P]),
+    "ubpl_conv1x1_forward_kmajor": (I, [P, I, I, I, P, P, I, P, P, P, P, P, P, P]),
     "ubpl_conv_weight_tapmajor": (I, [P, I, I, I, P, P]),
     "ubpl_conv2d_wgrad_workspace": (L, [I, I, I, I, I, I]),
     "ubpl_conv2d_wgrad": (I, [P, P, I, I, I, I, I, I, I, P, P, I, I, P, P, P, I, P]),
@@ -48,7 +51,7 @@ SIGNATURES = {
     "ubpl_conv_weights_split": (I, [P, P, L, P, I, I, I, P]),
     "ubpl_split_activation": (I, [P, I, I, I, I, P, P, I, I, P, L, P]),
     "ubpl_conv2d_forward_psa_workspace": (L, [I, I, I, I, I, I, I]),
-    "ubpl_conv2d_forward_psa": (I, [P, L, I, I, I, I, I, P, L, P, I, I, P, P, P, I, P]),
+    "ubpl_conv2d_forward_psa": (I, [P, L, I, I, I, I, I, P, L, P, I, I, P, P, P, I, P, P]),
     "ubpl_maxpool2x2_forward": (I, [P, L, I, I, P, P]),
     "ubpl_maxpool2x2_backward": (I, [P, P, L, I, I, P, I, P]),
     "ubpl_avgpool2x2_forward": (I, [P, L, I, I, P, P]),

@@ -444,29 +444,47 @@ class _Exec:
             rm, rv = self.m.stats(b)
             Kn.bn_eval_coeffs(self.m.P(b + ".weight"), self.m.P(b + ".bias"), rm, rv, BN_EPS, sc, sh)
 
-    def bn(self, name, x):
-        """Train: batch statistics (+ running-stat update); eval: precomputed."""
+    def bn(self, name, x, part=None):
+        """Train: batch statistics (+ running-stat update) — from the partials
+        the producing conv wrote (part = (buffer, shift)) or by a pass over x;
+        eval: precomputed."""
         sc, sh, mu, istd = self.bnc(name)
         if self.train:
             rm, rv = self.m.stats(name)
-            Kn.bn_forward_stats(x, self.m.P(name + ".weight"), self.m.P(name + ".bias"), BN_EPS, BN_MOMENTUM, rm,
-                                rv, self.part, mu, istd, sc, sh)
+            g, b = self.m.P(name + ".weight"), self.m.P(name + ".bias")
+            if part is not None:
+                Kn.bn_stats_from_partials(part, x.shape[1], x.shape[0] * x[0, 0].numel(), g, b, BN_EPS,
+                                          BN_MOMENTUM, rm, rv, mu, istd, sc, sh)
+            else:
+                Kn.bn_forward_stats(x, g, b, BN_EPS, BN_MOMENTUM, rm, rv, self.part, mu, istd, sc, sh)
         return sc, sh
 
-    def conv(self, name, x, stride=1, pro=None, res=None, out=None):
+    def conv(self, name, x, stride=1, pro=None, res=None, out=None, stats=False):
+        """stats=True: also return the BatchNorm partials of the output for the
+        BN that consumes it — (y, (buffer, shift)) from the conv epilogue where
+        the kernel has one, (y, None) otherwise."""
+        y, part = self._conv(name, x, stride, pro, res, out, stats and self.train)
+        return (y, part) if stats else y
+
+    def _conv(self, name, x, stride, pro, res, out, stats):
         w = self.m.P(name + ".weight")
         b = self.m.P(name + ".bias")
         ps, ph = (None, None) if pro is None else pro
+        B, Cout = x.shape[0], w.shape[0]
+        mkpart = lambda: Kn.bn_partial_buffer(Cout, B * x.shape[2] * x.shape[3], x.device) if stats else None
         ws = self.m.SW(0, name + ".weight") if stride == 1 else None
         if ws is not None:
             if ws.npieces == 3:
+                part = mkpart()
                 xs = Kn.split_activation(x, 3, (ws.shape[1] == 9) * 1, ps, ph)
-                return Kn.conv2d_forward_psa(xs, ws, b, res=res, out=out)
-            return Kn.conv2d_forward_split(x, ws, b, ps, ph, res=res, out=out)
+                return Kn.conv2d_forward_psa(xs, ws, b, res=res, out=out, stat_part=part), part
+            return Kn.conv2d_forward_split(x, ws, b, ps, ph, res=res, out=out), None
         if w.shape[2] == 1 and stride == 1 and Kn.conv1x1_kmajor_ok(x, w.shape[0]):
-            return Kn.conv1x1_forward_kmajor(x, self.m.W(1, name + ".weight"), b, ps, ph, res=res, out=out)
+            part = mkpart()
+            return Kn.conv1x1_forward_kmajor(x, self.m.W(1, name + ".weight"), b, ps, ph, res=res, out=out,
+                                             stat_part=part), part
         wt = self.m.W(0, name + ".weight") if w.shape[2] > 1 else None
-        return Kn.conv2d_forward(x, w, b, stride, ps, ph, res=res, out=out, w_tap=wt)
+        return Kn.conv2d_forward(x, w, b, stride, ps, ph, res=res, out=out, w_tap=wt), None
 
     # ---- layers
     def stem(self, imgs):
@@ -488,10 +506,10 @@ class _Exec:
         cin = x.shape[1]
         cout = self.m._offs[p + ".conv3.conv.weight"][2][0]
         c1 = self.bn(p + ".bn1", x)
-        t1 = self.conv(p + ".conv1.conv", x, pro=c1)
-        c2 = self.bn(p + ".bn2", t1)
-        t2 = self.conv(p + ".conv2.conv", t1, pro=c2)
-        c3 = self.bn(p + ".bn3", t2)
+        t1, part = self.conv(p + ".conv1.conv", x, pro=c1, stats=True)
+        c2 = self.bn(p + ".bn2", t1, part)
+        t2, part = self.conv(p + ".conv2.conv", t1, pro=c2, stats=True)
+        c3 = self.bn(p + ".bn3", t2, part)
         if cin != cout:
             r = self.conv(p + ".skip_layer.conv", x)
             out = self.conv(p + ".conv3.conv", t2, pro=c3, res=r, out=r)

@@ -227,6 +227,21 @@ def bn_apply(x, scale, shift, relu, out=None):
     return y
 
 
+def bn_partial_buffer(C, N, device):
+    return torch.empty(int(_lib.lib().ubpl_bn_partial_floats(C, N)), device=device, dtype=F32)
+
+
+def bn_partials(y, part):
+    B, C = y.shape[:2]
+    call("ubpl_bn_partials", _p(y), B, C, y[0, 0].numel(), _p(part), stream())
+    return part
+
+
+def bn_stats_from_partials(part, C, N, gamma, beta, eps, momentum, rmean, rvar, mean, invstd, scale, shift_out):
+    call("ubpl_bn_stats_from_partials", _p(part), C, int(N), _p(gamma), _p(beta), float(eps), float(momentum),
+         _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift_out), stream())
+
+
 def bn_backward(dz, x, gamma, mean, invstd, scale, shift, relu, part, coef, dgamma, dbeta, add1=None, add2=None,
                 out=None):
     B, C = x.shape[:2]
@@ -278,16 +293,17 @@ def conv1x1_kmajor_ok(x, cout):
     return cout % 4 == 0 and (x.shape[2] * x.shape[3]) % 4 == 0 and x.data_ptr() % 16 == 0
 
 
-def conv1x1_forward_kmajor(x, wk, bias, pscale=None, pshift=None, res=None, out=None):
+def conv1x1_forward_kmajor(x, wk, bias, pscale=None, pshift=None, res=None, out=None, stat_part=None):
     """1x1 stride-1 conv with k-major weights wk (Cin*Cout floats, [Cin][Cout]):
-    y = conv(relu(x*pscale + pshift) or x) + bias (+ res; res may alias out)."""
+    y = conv(relu(x*pscale + pshift) or x) + bias (+ res; res may alias out);
+    stat_part: BatchNorm partials of y (bn_partial_buffer)."""
     B, Cin, H, W = x.shape
     Cout = wk.numel() // Cin
     y = torch.empty((B, Cout, H, W), device=x.device, dtype=F32) if out is None else out
     nws = _lib.lib().ubpl_conv1x1_kmajor_workspace(B, Cin, Cout, H * W)
     slab = torch.empty(int(nws), device=x.device, dtype=F32) if nws > 0 else None
     call("ubpl_conv1x1_forward_kmajor", _p(x), B, Cin, H * W, _p(wk), _p(bias), Cout, _p(pscale), _p(pshift),
-         _p(res), _p(y), _p(slab), stream())
+         _p(res), _p(y), _p(slab), _p(stat_part), stream())
     return y
 
 
@@ -404,8 +420,9 @@ def split_activation(x, npieces, pad, pscale=None, pshift=None, out=None):
     return SplitAct(out, plane, B, C, H, W, pad, npieces)
 
 
-def conv2d_forward_psa(xs, ws, bias, res=None, out=None):
-    """Stride-1 conv of pre-split activations xs (SplitAct) with SplitWeights ws."""
+def conv2d_forward_psa(xs, ws, bias, res=None, out=None, stat_part=None):
+    """Stride-1 conv of pre-split activations xs (SplitAct) with SplitWeights ws;
+    stat_part: BatchNorm partials of the output (bn_partial_buffer)."""
     Cout, T, wc = ws.shape
     KS = int(round(T ** 0.5))
     if wc != xs.C or ws.npieces != xs.npieces:
@@ -415,7 +432,7 @@ def conv2d_forward_psa(xs, ws, bias, res=None, out=None):
     nws = _lib.lib().ubpl_conv2d_forward_psa_workspace(B, xs.C, Cout, KS, H, W, ws.npieces)
     slab = torch.empty(int(nws), device=xs.buf.device, dtype=F32) if nws > 0 else None
     call("ubpl_conv2d_forward_psa", _p(xs.buf), int(xs.plane), B, xs.C, H, W, int(xs.pad), ws.ptr(), int(ws.plane),
-         _p(bias), Cout, KS, _p(res), _p(y), _p(slab), int(ws.npieces), stream())
+         _p(bias), Cout, KS, _p(res), _p(y), _p(slab), int(ws.npieces), _p(stat_part), stream())
     return y
 
 
