@@ -304,28 +304,29 @@ constexpr int CNT_DOUBLES = MAXBN / 2;
 // ---- statistics from 64-pixel partials (conv-epilogue fused: common.h
 // tile_bn_partials; or bn_partials_kernel below).  part [C][np][2] f32 =
 // (S, M2) per slice, Chan's parallel form.
+// One wave per (channel, 64-pixel slice): lane = pixel (coalesced along p),
+// S and M2 by wave reductions.  4 waves per block.
 __global__ void __launch_bounds__(256) bn_partials_kernel(const float* __restrict__ y, int C, int P, int64_t N,
                                                          float* __restrict__ part) {
     const int64_t np = (N + 63) / 64;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (c, q)
-    if (i >= (int64_t)C * np) return;
-    const int c = (int)(i / np);
-    const int64_t q = i - (int64_t)c * np;
-    const int64_t n1 = min(N, q * 64 + 64);
-    float s = 0.f;
-    for (int64_t n = q * 64; n < n1; ++n) {
-        const int64_t b = n / P;
-        s += y[(b * C + c) * P + (n - b * P)];
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // (c, q)
+    if (w >= (int64_t)C * np) return;
+    const int lane = threadIdx.x & 63;
+    const int c = (int)(w / np);
+    const int64_t q = w - (int64_t)c * np;
+    const int64_t n = q * 64 + lane;
+    const bool ok = n < N;
+    const int64_t nc = ok ? n : N - 1;
+    const int64_t b = nc / P;
+    const float v = y[(b * C + c) * P + (nc - b * P)];
+    const float cnt = (float)(N - q * 64 < 64 ? N - q * 64 : 64);
+    const float s = ubpl::wave_sum(ok ? v : 0.f);
+    const float d = ok ? v - s / cnt : 0.f;
+    const float m2 = ubpl::wave_sum(d * d);
+    if (lane == 0) {
+        part[w * 2] = s;
+        part[w * 2 + 1] = m2;
     }
-    const float mu = s / (float)(n1 - q * 64);
-    float m2 = 0.f;
-    for (int64_t n = q * 64; n < n1; ++n) {
-        const int64_t b = n / P;
-        const float d = y[(b * C + c) * P + (n - b * P)] - mu;
-        m2 = fmaf(d, d, m2);
-    }
-    part[i * 2] = s;
-    part[i * 2 + 1] = m2;
 }
 
 // mean = sum S / N; M2 = sum M2_q + sum n_q (S_q/n_q - mean)^2, in f64.
@@ -370,7 +371,7 @@ UBPL_API int64_t ubpl_bn_partial_floats(int C, int64_t N) { return 2 * (int64_t)
 UBPL_API int ubpl_bn_partials(const float* y, int B, int C, int P, float* part, void* stream) {
     const int64_t N = (int64_t)B * P;
     const int64_t n = (int64_t)C * ((N + 63) / 64);
-    hipLaunchKernelGGL(bn_partials_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, y, C,
+    hipLaunchKernelGGL(bn_partials_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, y, C,
                        P, N, part);
     UBPL_LAUNCH_CHECK();
     return 0;
