@@ -146,6 +146,10 @@ int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, int H, in
  * transposed kernel ([Cin][Cout/G][T][G], G from Cout), so
  * dx = ubpl_conv2d_forward(dy, wt). */
 int ubpl_conv_weight_flip(const float* w, int Cout, int Cin, int KS, float* wt, void* stream);
+/* Reduce a weight-gradient slab [splits][Cout][Cin*T + 1] (columns n = tap*Cin + ci,
+ * last = bias) into dw (reference layout, (+)=) and db (nullable). */
+int ubpl_wgrad_slab_reduce(const float* slab, int splits, int Cout, int Cin, int T, int with_bias, float* dw,
+                           float* db, int accumulate, void* stream);
 /* Both re-layouts for many convs in one launch: table int64 [nseg][5] =
  * (src_off, dst_off, Cout, Cin, KS*KS) in floats; mode 0 tap-major, 1 dgrad. */
 int ubpl_conv_weights_relayout(const float* src, float* dst, const int64_t* table, int nseg, int mode, void* stream);
@@ -173,6 +177,13 @@ int ubpl_split_activation(const float* x, int B, int C, int H, int W, const floa
 /* Stride-1 conv (KS 1 or 3) of PSA activations (pad >= (KS-1)/2) with split
  * weights: both operands DMA'd global -> LDS; y = conv + bias (+ res, may alias y). */
 int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int KS, int H, int W, int npieces);
+/* 3x3 weight gradient (+ bias gradient, db nullable) on the split path from PSA
+ * operands with a 1-pixel border: dys = split(dy), xs = split(conv input),
+ * npieces = 3; Cin % 128 == 0, Cout % 128 == 0, W % 16 == 0. */
+int64_t ubpl_wgrad3_psa_workspace(int B, int Cin, int Cout, int H, int W);
+int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int Cin,
+                    int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,
+                    void* stream);
 int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                             const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
                             const float* res, float* y, float* slab, int npieces, float* stat_part, void* stream);

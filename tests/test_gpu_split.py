@@ -159,3 +159,32 @@ def test_split_activation_layout():
     ref = torch.zeros(2, 2, 7, 9, 16, dtype=torch.float64)
     ref[:, :, 1:6, 1:8, :] = v.view(2, 2, 16, 5, 7).permute(0, 1, 3, 4, 2)
     assert torch.equal(tot, ref)
+
+
+@pytest.mark.parametrize("case", [(2, 128, 128, 64, 64), (3, 128, 128, 16, 32), (2, 256, 128, 32, 16),
+                                  (2, 128, 256, 16, 16)])
+def test_wgrad3_psa_vs_f64(case):
+    """3x3 weight + bias gradient from PSA operands (transposed LDS reads,
+    split-K slab) within 2x the exact-f32 kernel's error against float64."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, Cout, H, W = case
+    gen = torch.Generator().manual_seed(41 + hash(case) % 1000)
+    x = torch.randn(B, Cin, H, W, generator=gen)
+    dy = torch.randn(B, Cout, H, W, generator=gen)
+    sc, sh = torch.rand(Cin, generator=gen) + 0.5, torch.randn(Cin, generator=gen) * 0.5
+    inp = F.relu((x.double() * sc.double()[None, :, None, None] + sh.double()[None, :, None, None]).float())
+    dwref = torch.nn.grad.conv2d_weight(inp.double(), (Cout, Cin, 3, 3), dy.double(), 1, 1)
+    dbref = dy.double().sum((0, 2, 3))
+    d = lambda t: t.to(DEV)
+    xs = Kn.split_activation(d(x), 3, 1, d(sc), d(sh))
+    ys = Kn.split_activation(d(dy), 3, 1)
+    assert Kn.wgrad3_psa_ok(ys, xs)
+    dw = torch.full((Cout, Cin, 3, 3), 0.25, device=DEV)
+    db = torch.full((Cout,), -0.5, device=DEV)
+    Kn.conv2d_wgrad3_psa(ys, xs, dw, db, accumulate=True)
+    dw32, db32 = torch.zeros(Cout, Cin, 3, 3, device=DEV), torch.zeros(Cout, device=DEV)
+    Kn.conv2d_wgrad(d(dy), d(x), 3, 1, dw32, db32, d(sc), d(sh), accumulate=False)
+    e32, esp = _rel(dw32, dwref), _rel(dw - 0.25, dwref)
+    print("wgrad3 %s: f32 %.2e split %.2e" % (case, e32, esp))
+    assert esp <= 2 * e32 + 1e-8, (esp, e32)
+    assert _rel(db + 0.5, dbref) <= 1e-5

@@ -1415,6 +1415,13 @@ UBPL_API int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, 
     return launch_wgrad_reduce(slab, splits, Cout, Cin, KS * KS, wb, dw, db, accumulate, st);
 }
 
+// Reduce a weight-gradient slab [splits][Cout][Cin*T + 1] (columns tap-major
+// n = tap*Cin + ci, the last = bias) into dw (reference layout) and db (nullable).
+UBPL_API int ubpl_wgrad_slab_reduce(const float* slab, int splits, int Cout, int Cin, int T, int with_bias, float* dw,
+                                    float* db, int accumulate, void* stream) {
+    return launch_wgrad_reduce(slab, splits, Cout, Cin, T, with_bias, dw, db, accumulate, (hipStream_t)stream);
+}
+
 // Forward weight layout: wt[co][ci/G][tap][ci%G] = w[co][ci][tap], G = 16 if it
 // divides Cin, else Cin (plain tap-major); for KS == 1 it is w itself.
 UBPL_API int ubpl_conv_weight_tapmajor(const float* w, int Cout, int Cin, int KS, float* wt, void* stream) {

@@ -23,6 +23,7 @@ using ubpl::xcd_remap;
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short short8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
@@ -519,6 +520,176 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
     }
 }
 
+// ------------------------------------------------------------------ 3x3 weight gradient
+// dW[co][tap][ci] = sum over (b, oh, ow) of dy[b,co,oh,ow] * x[b,ci,oh+kh-1,ow+kw-1]
+// on the split path, both operands in the PSA layout with a 1-pixel border
+// (dy: the data gradient's own pre-split operand; x: the forward's pre-split
+// conv input = relu(bn(t1)), kept for the backward).  GEMM: M = co, N = (tap,
+// ci) tap-major (n-tile = one tap x 128 channels), K = pixels, K step = 16
+// consecutive pixels of one output row (W % 16 == 0), split over workgroups
+// into a slab [z][Cout][9*Cin + 1] reduced by conv.hip's wgrad_reduce_kernel
+// (last column: the bias gradient, summed by the tap-0 workgroups).
+// The MFMA wants 8 consecutive pixels of one channel per lane, the PSA image
+// holds 16 channels per pixel: fragments come from LDS by
+// ds_read_b64_tr_b16 (a 16-lane group reads a 4-pixel x 16-channel block,
+// lane i gets channel i's 4 pixels), two per 8-bf16 fragment.  LDS stage
+// image [piece][16-channel group][16 pixel rows][32 B]; odd groups store
+// pixel rows 0-3 <-> 4-7 swapped (pre-permuted DMA source) so the two groups a
+// 32-lane half reads sit in opposite 128-B bank halves.
+template <int NP>
+__global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __restrict__ dys, int64_t dplane,
+                                                          const uint16_t* __restrict__ xs, int64_t xplane, int B,
+                                                          int Cin, int Cout, int H, int W, int steps_per_split,
+                                                          float* __restrict__ slab) {
+    constexpr int BM = 128, TM = 2, TN = 2, NS = 3;
+    constexpr int AB = NP * 8 * 512, BB = NP * 8 * 512;   // bytes per stage: 8 groups x 16 px x 32 B per piece
+    __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
+    typedef short v4i16 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4i16* tr_ptr_t;
+
+    const int Hp = H + 2, Wp = W + 2;
+    const int Gci = Cin >> 4, Gco = Cout >> 4;
+    const int Ntot = 9 * Cin, Nt = Ntot + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+    // tile order: n tiles (tap, ci) fastest so the 9 taps of one K split share an L2
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                              gridDim.x * gridDim.y * gridDim.z);
+    const int bx = lam % gridDim.x, by = (lam / gridDim.x) % gridDim.y, bz = lam / (gridDim.x * gridDim.y);
+    const int m0 = by * BM;
+    const int ntile_per_tap = Cin / 128;
+    const int tap = bx / ntile_per_tap, ci0 = (bx - tap * ntile_per_tap) * 128;
+    const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+    const int wsteps = W >> 4;
+    const int total_steps = B * H * wsteps;
+    const int s_begin = bz * steps_per_split;
+    const int s_end = min(total_steps, s_begin + steps_per_split);
+    const int nkt = max(0, s_end - s_begin);
+
+    // DMA lane geometry: wave w moves channel groups 2w, 2w+1 of both operands
+    const int gl = 2 * wid + (lane >> 5);
+    const int rphys = (lane & 31) >> 1;
+    const int rlog = rphys ^ (4 * (gl & 1));
+    const int64_t HWp = (int64_t)Hp * Wp;
+    const int64_t a_lane = (((int64_t)(m0 >> 4) + gl) * HWp + rlog) * 16 + 8 * (lane & 1);
+    const int64_t b_lane = (((int64_t)(ci0 >> 4) + gl) * HWp + rlog) * 16 + 8 * (lane & 1);
+    auto stage = [&](int buf, int s) {
+        const int b = s / (H * wsteps);
+        const int rem = s - b * (H * wsteps);
+        const int oh = rem / wsteps, ow0 = (rem - oh * wsteps) * 16;
+        const int64_t aoff = (int64_t)b * Gco * HWp * 16 + ((int64_t)(oh + 1) * Wp + ow0 + 1) * 16;
+        const int64_t boff = (int64_t)b * Gci * HWp * 16 + ((int64_t)(oh + kh) * Wp + ow0 + kw) * 16;
+        char* base = lds + buf * (AB + BB);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(dys + p * dplane + aoff + a_lane),
+                                             (lds_ptr_t)(base + p * 4096 + wid * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(xs + p * xplane + boff + b_lane),
+                                             (lds_ptr_t)(base + AB + p * 4096 + wid * 1024), 16, 0, 0);
+        }
+    };
+
+    // transposed-read geometry: 16-lane group g reads channel group (tile base
+    // + (g & 1)), pixel rows 8*(g >> 1) + 4t + q (q = i16 >> 2), columns 4*(i16 & 3)
+    const int g16 = lane >> 4, i16 = lane & 15;
+    const int qrow = i16 >> 2, pcol = i16 & 3;
+    auto tr_off = [&](int grp, int t) {   // byte offset inside a piece image
+        const int row = (8 * (g16 >> 1) + 4 * t + qrow) ^ (4 * (grp & 1));
+        return grp * 512 + row * 32 + 8 * pcol;
+    };
+    int aoffs[TM][2], boffs[TN][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) aoffs[i][t] = tr_off((wm + 32 * i) / 16 + (g16 & 1), t);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) boffs[j][t] = tr_off((wn + 32 * j) / 16 + (g16 & 1), t);
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const bool bias_wave = bx == 0 && wn == 0;
+    float bsum[TM] = {};
+
+    if (nkt > 0) stage(0, s_begin);
+    if (nkt > 1) stage(1, s_begin + 1);
+    for (int t = 0; t < nkt; ++t) {
+        if (t + 1 < nkt) vm_wait<2 * NP>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + 2 < nkt) stage((t + 2) % NS, s_begin + t + 2);
+        char* base = lds + (t % NS) * (AB + BB);
+        bf16x8 af[TM][NP], bfr[TN][NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * 4096 + aoffs[i][0]));
+                const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * 4096 + aoffs[i][1]));
+                const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                af[i][p] = __builtin_bit_cast(bf16x8, v);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const v4i16 lo =
+                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * 4096 + boffs[j][0]));
+                const v4i16 hi =
+                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * 4096 + boffs[j][1]));
+                const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                bfr[j][p] = __builtin_bit_cast(bf16x8, v);
+            }
+        }
+        if (bias_wave) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int p = 0; p < NP; ++p)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) bsum[i] += (float)af[i][p][e];
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                floatx16 tmp;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) tmp[r] = 0.f;
+                mfma_split<NP>(tmp, af[i], bfr[j]);
+                acc[i][j] += tmp;
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    float* sl = slab + (int64_t)bz * Cout * Nt;
+    const int li = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = tap * Cin + ci0 + wn + 32 * j + li;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                sl[(int64_t)m * Nt + n] = acc[i][j][r];
+            }
+    }
+    if (bias_wave) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            // lane (r, h) summed channel wm + 32i + r over pixels 8h..8h+7 of each step
+            const float v = bsum[i] + __shfl_xor(bsum[i], 32, 64);
+            if (h == 0) sl[(int64_t)(m0 + wm + 32 * i + li) * Nt + Ntot] = v;
+        }
+    }
+}
+
 // y[b,m,p] = sum_z slab[z][m][b*P+p] + bias[m] (+ res)
 __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restrict__ slab, int splits, int Cout, int P,
                                                           int64_t N, const float* __restrict__ bias, const float* res,
@@ -846,4 +1017,42 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
 #undef UBPL_PS_BM
 #undef UBPL_PS
     return (int)hipErrorInvalidValue;
+}
+
+// ---- 3x3 weight gradient on the split path
+namespace {
+int wgrad3_splits(int B, int Cin, int Cout, int H, int W) {
+    const int tiles = 9 * (Cin / 128) * (Cout / 128);
+    const int steps = B * H * (W / 16);
+    int s = (512 + tiles / 2) / tiles;                 // ~one round of 2 workgroups per CU
+    if (s < 1) s = 1;
+    if (s > steps / 8) s = steps / 8 > 0 ? steps / 8 : 1;   // >= 8 K steps per split
+    const int per = (steps + s - 1) / s;
+    return (steps + per - 1) / per;
+}
+}  // namespace
+
+UBPL_API int64_t ubpl_wgrad3_psa_workspace(int B, int Cin, int Cout, int H, int W) {
+    if (Cin % 128 || Cout % 128 || W % 16) return 0;
+    return (int64_t)wgrad3_splits(B, Cin, Cout, H, W) * Cout * (9 * Cin + 1);
+}
+
+// dw[Cout,Cin,3,3] (+)= 3x3 weight gradient, db[Cout] (+)= sum dy (nullable), from
+// PSA operands with a 1-pixel border: dys = split(dy) [B][Cout/16][H+2][W+2][16],
+// xs = split(conv input) [B][Cin/16][H+2][W+2][16], npieces = 3.  Needs
+// Cin % 128 == 0, Cout % 128 == 0, W % 16 == 0.  slab: ubpl_wgrad3_psa_workspace floats.
+UBPL_API int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int Cin,
+                             int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,
+                             void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (Cin % 128 || Cout % 128 || W % 16 || npieces != 3 || slab == nullptr) return (int)hipErrorInvalidValue;
+    if ((((uintptr_t)dys) & 15) || (((uintptr_t)xs) & 15) || (dplane % 8) || (xplane % 8)) return (int)hipErrorInvalidValue;
+    const int splits = wgrad3_splits(B, Cin, Cout, H, W);
+    const int steps = B * H * (W / 16);
+    const int per = (steps + splits - 1) / splits;
+    dim3 grid((unsigned)(9 * (Cin / 128)), (unsigned)(Cout / 128), (unsigned)splits);
+    hipLaunchKernelGGL((wgrad3_psa_kernel<3>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout, H, W, per,
+                       slab);
+    UBPL_LAUNCH_CHECK();
+    return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 9, db != nullptr, dw, db, accumulate, stream);
 }

@@ -420,6 +420,7 @@ class _Exec:
     def __init__(self, model, B, dev, part, train, save):
         self.m, self.B, self.dev, self.part, self.train, self.do_save = model, B, dev, part, train, save
         self.saved = {}
+        self.saved_split = {}
         C = sum(self.m._offs[b + ".weight"][1] for b in self.m._bn_names)
         self.coef = torch.empty(4 * C, device=dev)     # per BN: scale|shift|mean|invstd
         self.cidx, o = {}, 0
@@ -477,6 +478,8 @@ class _Exec:
             if ws.npieces == 3:
                 part = mkpart()
                 xs = Kn.split_activation(x, 3, (ws.shape[1] == 9) * 1, ps, ph)
+                if self.do_save and ws.shape[1] == 9:
+                    self.saved_split[name] = xs          # the 3x3 weight gradient's B operand
                 return Kn.conv2d_forward_psa(xs, ws, b, res=res, out=out, stat_part=part), part
             return Kn.conv2d_forward_split(x, ws, b, ps, ph, res=res, out=out), None
         if w.shape[2] == 1 and stride == 1 and Kn.conv1x1_kmajor_ok(x, w.shape[0]):
@@ -564,8 +567,18 @@ class _Exec:
         self.wgrad(p + ".conv3.conv", dout, t2, 1, pro=c3)
         d = self.dgrad(p + ".conv3.conv", dout)                       # d relu(bn3(t2))
         d = self.bn_bwd(p + ".bn3", d, t2, relu=1)                     # d t2
-        self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
-        d = self.dgrad(p + ".conv2.conv", d)                           # d relu(bn2(t1))
+        ws = self.m.SW(1, p + ".conv2.conv.weight")
+        xs = self.saved_split.get(p + ".conv2.conv")
+        if ws is not None and ws.npieces == 3:
+            ys = Kn.split_activation(d, 3, 1)          # shared by the weight and data gradients
+            if xs is not None and Kn.wgrad3_psa_ok(ys, xs):
+                Kn.conv2d_wgrad3_psa(ys, xs, self.m.G(p + ".conv2.conv.weight"), self.m.G(p + ".conv2.conv.bias"))
+            else:
+                self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
+            d = Kn.conv2d_forward_psa(ys, ws, None)                    # d relu(bn2(t1))
+        else:
+            self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
+            d = self.dgrad(p + ".conv2.conv", d)                       # d relu(bn2(t1))
         d = self.bn_bwd(p + ".bn2", d, t1, relu=1)                     # d t1
         self.wgrad(p + ".conv1.conv", d, x, 1, pro=c1)
         d = self.dgrad(p + ".conv1.conv", d)                           # d relu(bn1(x))

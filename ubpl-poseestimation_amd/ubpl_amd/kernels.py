@@ -436,6 +436,19 @@ def conv2d_forward_psa(xs, ws, bias, res=None, out=None, stat_part=None):
     return y
 
 
+def wgrad3_psa_ok(ys, xs):
+    return (ys.npieces == 3 and xs.npieces == 3 and ys.pad == 1 and xs.pad == 1 and xs.C % 128 == 0
+            and ys.C % 128 == 0 and xs.W % 16 == 0 and (ys.B, ys.H, ys.W) == (xs.B, xs.H, xs.W))
+
+
+def conv2d_wgrad3_psa(ys, xs, dw, db, accumulate=True):
+    """3x3 weight (+ bias) gradient from PSA operands: ys = split(dy), xs = split(conv input), pad 1."""
+    n = _lib.lib().ubpl_wgrad3_psa_workspace(xs.B, xs.C, ys.C, xs.H, xs.W)
+    slab = torch.empty(int(n), device=xs.buf.device, dtype=F32)
+    call("ubpl_wgrad3_psa", _p(ys.buf), int(ys.plane), _p(xs.buf), int(xs.plane), xs.B, xs.C, ys.C, xs.H, xs.W,
+         _p(slab), _p(dw), _p(db), int(accumulate), 3, stream())
+
+
 def conv2d_dgrad(dy, w, res=None, out=None, wt=None):
     """dx of a stride-1 conv = conv(dy, flip(w)^T); res/out allow accumulation."""
     if wt is None:
