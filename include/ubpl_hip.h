@@ -132,7 +132,8 @@ int ubpl_conv_weight_tapmajor(const float* w, int Cout, int Cin, int KS, float* 
 /* 1x1 stride-1 conv fed by LDS-DMA, k-major weights wk [Cin][Cout] (the
  * data-gradient re-layout of the conv; for a data gradient, the reference
  * weights themselves): same semantics as ubpl_conv2d_forward with KS = 1.
- * Cout % 4 == 0, P % 4 == 0, x / wk 16-B aligned, Cin <= 256 with a prologue. */
+ * Cin % 16 == 0, Cout % 4 == 0, P % 4 == 0, x / wk 16-B aligned, Cin <= 256 with a
+ * prologue. */
 int64_t ubpl_conv1x1_kmajor_workspace(int B, int Cin, int Cout, int P);
 int ubpl_conv1x1_forward_kmajor(const float* x, int B, int Cin, int P, const float* wk, const float* bias, int Cout,
                                 const float* pscale, const float* pshift, const float* res, float* y, float* slab,

@@ -378,28 +378,32 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_dma_kernel(const float* __restr
     const int a_row = lane / (BM / 4);
     const int a_col = min(m0 + 4 * (lane % (BM / 4)), M - 4);
     const int b_row = lane >> 5;
-    int64_t b_off;   // offset of (b, k=0, p) in x
+    // per-lane 32-bit byte offsets over wave-uniform bases (scalar + vector
+    // addressing).  K % 16 == 0 (checked by the entry point): every DMA row is
+    // a real k row.
+    const uint32_t a_lane = (uint32_t)((a_row * M + a_col) * 4);
+    uint32_t b_lane;
     {
         int64_t n = n0 + 4 * (lane & 31);
         n = n < N ? n : N - 4;
         const int64_t b = n / P;
-        b_off = b * K * P + (n - b * P);
+        b_lane = (uint32_t)((b * K * P + (n - b * P) + (int64_t)b_row * P) * 4);
     }
     auto stage = [&](int buf, int kt) {
         char* base = lds + buf * (AB + BB);
 #pragma unroll
         for (int i = 0; i < A_PW; ++i) {
             const int q = wid * A_PW + i;
-            const int k = min(kt + q * A_RPI + a_row, K - 1);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(wk + (int64_t)k * M + a_col), (lds_ptr_t)(base + q * 1024),
-                                             16, 0, 0);
+            const int k0 = min(kt + q * A_RPI, K - A_RPI);
+            const char* ab = reinterpret_cast<const char*>(wk + (int64_t)k0 * M);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane), (lds_ptr_t)(base + q * 1024), 16, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < B_PW; ++i) {
             const int q = wid * B_PW + i;
-            const int k = min(kt + 2 * q + b_row, K - 1);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(x + b_off + (int64_t)k * P),
-                                             (lds_ptr_t)(base + AB + q * 1024), 16, 0, 0);
+            const int k0 = min(kt + 2 * q, K - 2);
+            const char* bb = reinterpret_cast<const char*>(x + (int64_t)k0 * P);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane), (lds_ptr_t)(base + AB + q * 1024), 16, 0, 0);
         }
     };
 
@@ -1295,7 +1299,7 @@ UBPL_API int64_t ubpl_conv1x1_kmajor_workspace(int B, int Cin, int Cout, int P) 
 // 1x1 stride-1 conv with k-major weights wk [Cin][Cout] (the data-gradient
 // re-layout of a 1x1 conv; for a data gradient, the reference weights
 // themselves): y[B,Cout,P] = conv(relu(x*pscale + pshift) or x) + bias (+ res,
-// may alias y).  Needs Cout % 4 == 0, P % 4 == 0, Cin <= 256 with a prologue,
+// may alias y).  Needs Cin % 16 == 0, Cout % 4 == 0, P % 4 == 0, Cin <= 256 with a prologue,
 // 16-B aligned x / wk.  slab: ubpl_conv1x1_kmajor_workspace floats (nullable at 0).
 // stat_part (nullable): BatchNorm partials of y (ubpl_bn_partials layout).
 UBPL_API int ubpl_conv1x1_forward_kmajor(const float* x, int B, int Cin, int P, const float* wk, const float* bias,
@@ -1303,7 +1307,8 @@ UBPL_API int ubpl_conv1x1_forward_kmajor(const float* x, int B, int Cin, int P, 
                                          float* y, float* slab, float* stat_part, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const bool pro = pscale != nullptr;
-    if ((pro && Cin > MAXC) || Cout % 4 != 0 || P % 4 != 0 || (((uintptr_t)x) & 15) || (((uintptr_t)wk) & 15))
+    if ((pro && Cin > MAXC) || Cin % BK != 0 || Cout % 4 != 0 || P % 4 != 0 || (((uintptr_t)x) & 15) ||
+        (((uintptr_t)wk) & 15))
         return (int)hipErrorInvalidValue;
     const Plan pl = fwd_plan(Cout, (int64_t)B * P, Cin, 128, true);
     if (pl.splits > 1 && slab == nullptr) return (int)hipErrorInvalidValue;

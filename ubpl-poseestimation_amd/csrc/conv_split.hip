@@ -383,15 +383,17 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
     const int lr = lane >> 1;
     const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
     const bool a_issue = wid < BM / 32;
-    const uint16_t* a_src = wp + (int64_t)min(m0 + 32 * wid + lr, Cout - 1) * Ktot + 8 * lchunk;
-    const uint16_t* b_src;
+    // per-lane 32-bit byte offsets over wave-uniform bases (scalar + vector
+    // addressing: no 64-bit VALU per DMA instruction)
+    const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, Cout - 1) * Ktot + 8 * lchunk) * 2);
+    uint32_t b_lane;
     {
         int64_t n = n0 + 32 * wid + lr;
         n = n < N ? n : N - 1;
         const int b = (int)(n / P);
         const int p = (int)(n - (int64_t)b * P);
         const int oh = p / W, ow = p - oh * W;
-        b_src = xs + (((int64_t)b * G * Hp + oh + pad - PADK) * Wp + ow + pad - PADK) * 16 + 8 * lchunk;
+        b_lane = (uint32_t)(((((int64_t)b * G * Hp + oh + pad - PADK) * Wp + ow + pad - PADK) * 16 + 8 * lchunk) * 2);
     }
     auto stage = [&](int buf, int kt) {
         const int kg = kt >> 4;
@@ -401,10 +403,12 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
         char* base = lds + buf * (AB + BB);
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
+            const char* ab = reinterpret_cast<const char*>(wp + p * wplane + kt);
+            const char* bb = reinterpret_cast<const char*>(xs + p * xplane + boff);
             if (a_issue)
-                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(a_src + p * wplane + kt),
+                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane),
                                                  (lds_ptr_t)(base + p * BM * 32 + wid * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(b_src + p * xplane + boff),
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
                                              (lds_ptr_t)(base + AB + p * BN * 32 + wid * 1024), 16, 0, 0);
         }
     };
@@ -571,8 +575,12 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
     const int rphys = (lane & 31) >> 1;
     const int rlog = rphys ^ (4 * (gl & 1));
     const int64_t HWp = (int64_t)Hp * Wp;
-    const int64_t a_lane = (((int64_t)(m0 >> 4) + gl) * HWp + rlog) * 16 + 8 * (lane & 1);
-    const int64_t b_lane = (((int64_t)(ci0 >> 4) + gl) * HWp + rlog) * 16 + 8 * (lane & 1);
+    // per-lane 32-bit byte offsets; the rest of each DMA address is wave-uniform
+    // (scalar base + vector offset addressing, no 64-bit VALU per instruction)
+    const uint32_t a_lane = (uint32_t)(((gl * HWp + rlog) * 16 + 8 * (lane & 1)) * 2);
+    const uint32_t b_lane = a_lane;
+    const char* dys_m = reinterpret_cast<const char*>(dys + (int64_t)(m0 >> 4) * HWp * 16);
+    const char* xs_c = reinterpret_cast<const char*>(xs + (int64_t)(ci0 >> 4) * HWp * 16);
     auto stage = [&](int buf, int s) {
         const int b = s / (H * wsteps);
         const int rem = s - b * (H * wsteps);
@@ -582,9 +590,11 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
         char* base = lds + buf * (AB + BB);
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(dys + p * dplane + aoff + a_lane),
-                                             (lds_ptr_t)(base + p * 4096 + wid * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(xs + p * xplane + boff + b_lane),
+            const char* ab = dys_m + 2 * (p * dplane + aoff);
+            const char* bb = xs_c + 2 * (p * xplane + boff);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane), (lds_ptr_t)(base + p * 4096 + wid * 1024), 16,
+                                             0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
                                              (lds_ptr_t)(base + AB + p * 4096 + wid * 1024), 16, 0, 0);
         }
     };
@@ -614,7 +624,9 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
         for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    const bool bias_wave = bx == 0 && wn == 0;
+    // the bias gradient of split z is summed by the tap (z % 9) workgroups (their
+    // first 128 input channels), spreading that VALU work over the taps
+    const bool bias_wave = tap == bz % 9 && ci0 == 0 && wn == 0;
     float bsum[TM] = {};
 
     if (nkt > 0) stage(0, s_begin);
@@ -1024,7 +1036,7 @@ namespace {
 int wgrad3_splits(int B, int Cin, int Cout, int H, int W) {
     const int tiles = 9 * (Cin / 128) * (Cout / 128);
     const int steps = B * H * (W / 16);
-    int s = (512 + tiles / 2) / tiles;                 // ~one round of 2 workgroups per CU
+    int s = 512 / tiles;                               // one round of 2 workgroups per CU, not one over
     if (s < 1) s = 1;
     if (s > steps / 8) s = steps / 8 > 0 ? steps / 8 : 1;   // >= 8 K steps per split
     const int per = (steps + s - 1) / s;

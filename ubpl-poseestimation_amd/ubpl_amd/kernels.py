@@ -289,8 +289,9 @@ def conv2d_forward(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out
 
 
 def conv1x1_kmajor_ok(x, cout):
-    """Shapes / alignment the LDS-DMA 1x1 kernel takes."""
-    return cout % 4 == 0 and (x.shape[2] * x.shape[3]) % 4 == 0 and x.data_ptr() % 16 == 0
+    """Shapes / alignment the LDS-DMA 1x1 kernel takes (x: its B operand)."""
+    return (x.shape[1] % 16 == 0 and cout % 4 == 0 and (x.shape[2] * x.shape[3]) % 4 == 0
+            and x.data_ptr() % 16 == 0)
 
 
 def conv1x1_forward_kmajor(x, wk, bias, pscale=None, pshift=None, res=None, out=None, stat_part=None):
