@@ -110,6 +110,13 @@ int ubpl_bn_partials(const float* y, int B, int C, int P, float* part, void* str
 int ubpl_bn_stats_from_partials(const float* part, int C, int64_t N, const float* gamma,
                                 const float* beta, float eps, float momentum, float* rmean, float* rvar,
                                 float* mean_out, float* invstd_out, float* scale, float* shift_out, void* stream);
+/* The same backward with dx delivered only as PSA planes (ubpl_split_activation
+ * layout, border `pad`, npieces 2 or 3) — the operand of a split-path 3x3 data /
+ * weight gradient; no addends; C % 16 == 0. */
+int ubpl_bn_backward_split(const float* dz, const float* x, int B, int C, int H, int W, const float* gamma,
+                           const float* mean, const float* invstd, const float* scale, const float* shift, int relu,
+                           double* part, float* coef, float* dgamma, float* dbeta, int pad, int npieces,
+                           uint16_t* dst, int64_t plane, void* stream);
 /* Backward of y = [relu](bn(x)); dgamma/dbeta accumulate; dx = add1 + add2 + dL/dx. */
 int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma, const float* mean,
                      const float* invstd, const float* scale, const float* shift, int relu, double* part,

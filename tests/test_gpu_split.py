@@ -188,3 +188,30 @@ def test_wgrad3_psa_vs_f64(case):
     print("wgrad3 %s: f32 %.2e split %.2e" % (case, e32, esp))
     assert esp <= 2 * e32 + 1e-8, (esp, e32)
     assert _rel(db + 0.5, dbref) <= 1e-5
+
+
+def test_bn_backward_split_matches_f32_then_split():
+    """bn_backward_split == split_activation(bn_backward(...)) bit for bit (same
+    per-element formula), dgamma/dbeta identical."""
+    from ubpl_amd import kernels as Kn
+    gen = torch.Generator().manual_seed(9)
+    B, C, H, W = 2, 32, 8, 16
+    d = lambda t: t.to(DEV)
+    dz, x = d(torch.randn(B, C, H, W, generator=gen)), d(torch.randn(B, C, H, W, generator=gen))
+    gamma = d(torch.rand(C, generator=gen) + 0.5)
+    mean, istd = d(torch.randn(C, generator=gen) * 0.1), d(torch.rand(C, generator=gen) + 0.5)
+    sc, sh = gamma * istd, d(torch.randn(C, generator=gen)) - mean * gamma * istd
+    part = torch.zeros(int(__import__("ubpl_amd")._lib.lib().ubpl_bn_part_doubles(B, C)), dtype=torch.float64,
+                       device=DEV)
+    outs = []
+    for mode in ("f32", "split"):
+        coef = torch.empty(3 * C, device=DEV)
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        if mode == "f32":
+            dx = Kn.bn_backward(dz, x, gamma, mean, istd, sc, sh, 1, part, coef, dg, db, out=torch.empty_like(dz))
+            ys = Kn.split_activation(dx, 3, 1)
+        else:
+            ys = Kn.bn_backward_split(dz, x, gamma, mean, istd, sc, sh, 1, part, coef, dg, db, 3, 1)
+        outs.append((ys.buf.cpu(), dg.cpu(), db.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -435,6 +435,75 @@ UBPL_API int ubpl_bn_apply(const float* x, int B, int C, int HW, const float* sc
 // Backward of y = [relu](bn(x)) given dz = dL/dy.  dgamma/dbeta are
 // ACCUMULATED (+=).  dx = add1 + add2 + dL/dx (add1/add2 nullable; dx may
 // alias dz, add1 or add2).  coef: scratch of 3*C floats.
+// dx of the BN backward written straight into the PSA layout (conv_split.hip
+// split_act_kernel's [B][C/16][H+2pad][W+2pad][16] bf16 planes, zero border):
+// one thread per padded pixel of one 16-channel group, like split_act.
+template <int NP>
+__global__ void __launch_bounds__(256) bwd_apply_split_kernel(const float* __restrict__ dz,
+                                                             const float* __restrict__ x, int C, int H, int W,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean, int relu,
+                                                             const float* __restrict__ ca,
+                                                             const float* __restrict__ cb,
+                                                             const float* __restrict__ cc, int pad,
+                                                             uint16_t* __restrict__ dst, int64_t plane) {
+    const int Hp = H + 2 * pad, Wp = W + 2 * pad, G = C >> 4;
+    const int b = blockIdx.z, g = blockIdx.y;
+    const int pix = blockIdx.x * 256 + threadIdx.x;
+    if (pix >= Hp * Wp) return;
+    const int hp = pix / Wp, wq = pix - hp * Wp;
+    const int h = hp - pad, w = wq - pad;
+    const bool in = h >= 0 && h < H && w >= 0 && w < W;
+    const int64_t HW = (int64_t)H * W;
+    const int64_t o = ((int64_t)b * C + 16 * g) * HW + (in ? h * W + w : 0);
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int c = 16 * g + j;
+        const float r = bwd_one(dz[o + j * HW], x[o + j * HW], scale[c], shift[c], mean[c], ca[c], cb[c], cc[c], relu);
+        v[j] = in ? r : 0.f;
+    }
+    ubpl::store_psa_row<NP>(v, dst + (((int64_t)(b * G + g) * Hp + hp) * Wp + wq) * 16, plane);
+}
+
+// ubpl_bn_backward with dx delivered as PSA planes only (no f32 dx, no
+// addends): statistics pass, then bwd_apply_split_kernel.  C % 16 == 0.
+UBPL_API int ubpl_bn_backward_split(const float* dz, const float* x, int B, int C, int H, int W, const float* gamma,
+                                    const float* mean, const float* invstd, const float* scale, const float* shift,
+                                    int relu, double* part, float* coef, float* dgamma, float* dbeta, int pad,
+                                    int npieces, uint16_t* dst, int64_t plane, void* stream) {
+    const int HW = H * W;
+    if (C % 16 != 0 || C > MAXBN || npieces < 2 || npieces > 3 || pad < 0) return (int)hipErrorInvalidValue;
+    const int splits = splits_for(B, C);
+    const int bper = (B + splits - 1) / splits;
+    const int gs = (B + bper - 1) / bper;
+    const bool vec = (HW % 4 == 0) && ((((uintptr_t)dz | (uintptr_t)x) & 15) == 0);
+    float* ca = coef;
+    float* cb = coef + C;
+    float* cc = coef + 2 * C;
+    unsigned* cnt = reinterpret_cast<unsigned*>(part);
+    part += CNT_DOUBLES;
+    const BwdOut o{gamma, invstd, dgamma, dbeta, ca, cb, cc};
+    if (vec)
+        hipLaunchKernelGGL(bwd_stats_kernel<true>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
+                           bper, scale, shift, mean, relu, part, cnt, o);
+    else
+        hipLaunchKernelGGL(bwd_stats_kernel<false>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
+                           bper, scale, shift, mean, relu, part, cnt, o);
+    UBPL_LAUNCH_CHECK();
+    const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+    dim3 grid((unsigned)((Hp * Wp + 255) / 256), (unsigned)(C / 16), (unsigned)B);
+    if (npieces == 3)
+        hipLaunchKernelGGL(bwd_apply_split_kernel<3>, grid, dim3(256), 0, (hipStream_t)stream, dz, x, C, H, W, scale,
+                           shift, mean, relu, ca, cb, cc, pad, dst, plane);
+    else
+        hipLaunchKernelGGL(bwd_apply_split_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream, dz, x, C, H, W, scale,
+                           shift, mean, relu, ca, cb, cc, pad, dst, plane);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
 UBPL_API int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma,
                               const float* mean, const float* invstd, const float* scale, const float* shift,
                               int relu, double* part, float* coef, float* dgamma, float* dbeta, const float* add1,

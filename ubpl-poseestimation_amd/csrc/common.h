@@ -80,6 +80,42 @@ __device__ __forceinline__ float block_max(float v, float* smem) {
 
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// Two floats -> NP packed bf16 pairs (piece p of a in the low half): the
+// split-bf16 representation v = v0 + v1 (+ v2), v_p = bf16(v - v_0 - ... - v_{p-1}).
+template <int NP>
+__device__ __forceinline__ void split2(float a, float b, uint32_t (&o)[NP]) {
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const __bf16 ha = (__bf16)a, hb = (__bf16)b;
+        const bf16x2_t v = {ha, hb};
+        o[p] = __builtin_bit_cast(uint32_t, v);
+        if (p + 1 < NP) {
+            a -= (float)ha;
+            b -= (float)hb;
+        }
+    }
+}
+
+// 16 channel values of one pixel -> the NP bf16 planes of a PSA image row
+// (conv_split.hip split_act_kernel layout): 32 contiguous bytes per plane.
+template <int NP>
+__device__ __forceinline__ void store_psa_row(const float (&v)[16], uint16_t* d, int64_t plane) {
+    uint32_t pk[NP][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t o[NP];
+        split2<NP>(v[2 * i], v[2 * i + 1], o);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) pk[p][i] = o[p];
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        *reinterpret_cast<uint4*>(d + p * plane) = make_uint4(pk[p][0], pk[p][1], pk[p][2], pk[p][3]);
+        *reinterpret_cast<uint4*>(d + p * plane + 8) = make_uint4(pk[p][4], pk[p][5], pk[p][6], pk[p][7]);
+    }
+}
+
 // Sum over the 32 lanes of each wave half by DPP row shifts (Hillis-Steele
 // within a 16-lane row, then row_bcast:15 into rows 1 and 3): the total of
 // lanes 0-31 lands in lane 31, of lanes 32-63 in lane 63.

@@ -31,20 +31,7 @@ constexpr int NT = 256;
 constexpr int BK = 32;
 constexpr int BN = 128;
 
-// Two floats -> NP packed bf16 pairs (piece p of a in the low half).
-template <int NP>
-__device__ __forceinline__ void split2(float a, float b, uint32_t (&o)[NP]) {
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        const __bf16 ha = (__bf16)a, hb = (__bf16)b;
-        const bf16x2 v = {ha, hb};
-        o[p] = __builtin_bit_cast(uint32_t, v);
-        if (p + 1 < NP) {
-            a -= (float)ha;
-            b -= (float)hb;
-        }
-    }
-}
+using ubpl::split2;
 
 __device__ __forceinline__ int swz(int row, int c) { return c ^ ((row >> 2) & 3); }
 
@@ -318,20 +305,7 @@ __global__ void __launch_bounds__(256) split_act_kernel(const float* __restrict_
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) v[j] = in ? v[j] : 0.f;
-    uint32_t pk[NP][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint32_t o[NP];
-        split2<NP>(v[2 * i], v[2 * i + 1], o);
-#pragma unroll
-        for (int p = 0; p < NP; ++p) pk[p][i] = o[p];
-    }
-    uint16_t* d = dst + (((int64_t)(b * G + g) * Hp + hp) * Wp + wq) * 16;
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        *reinterpret_cast<uint4*>(d + p * plane) = make_uint4(pk[p][0], pk[p][1], pk[p][2], pk[p][3]);
-        *reinterpret_cast<uint4*>(d + p * plane + 8) = make_uint4(pk[p][4], pk[p][5], pk[p][6], pk[p][7]);
-    }
+    ubpl::store_psa_row<NP>(v, dst + (((int64_t)(b * G + g) * Hp + hp) * Wp + wq) * 16, plane);
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -476,20 +450,30 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                 bfr[j][p] = *reinterpret_cast<const bf16x8*>(base + AB + p * BN * 32 + row * 32 +
                                                             16 * (h ^ ((row >> 3) & 1)));
         }
+        if constexpr (NP == 3) {
+            // every tile's chunk chain first, the f32 adds after them (behind a
+            // scheduling barrier): an add right behind its own chain waits out
+            // the MFMA latency (s_nop) with the other tiles' chains not issued
+            floatx16 tmp[TM][TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                if constexpr (NP == 3) {
-                    floatx16 tmp;
+                for (int j = 0; j < TN; ++j) {
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) tmp[r] = 0.f;
-                    mfma_split<NP>(tmp, af[i], bfr[j]);
-                    acc[i][j] += tmp;
-                } else {
-                    mfma_split<NP>(acc[i][j], af[i], bfr[j]);
+                    for (int r = 0; r < 16; ++r) tmp[i][j][r] = 0.f;
+                    mfma_split<NP>(tmp[i][j], af[i], bfr[j]);
                 }
-            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] += tmp[i][j];
+        } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) mfma_split<NP>(acc[i][j], af[i], bfr[j]);
+        }
         // fragments consumed (the MFMAs waited on them) before the next barrier
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -666,16 +650,20 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
 #pragma unroll
                     for (int e = 0; e < 8; ++e) bsum[i] += (float)af[i][p][e];
         }
+        floatx16 tmp[TM][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                floatx16 tmp;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) tmp[r] = 0.f;
-                mfma_split<NP>(tmp, af[i], bfr[j]);
-                acc[i][j] += tmp;
+                for (int r = 0; r < 16; ++r) tmp[i][j][r] = 0.f;
+                mfma_split<NP>(tmp[i][j], af[i], bfr[j]);
             }
+        __builtin_amdgcn_sched_barrier(0);   // chains first, adds after (see conv_psa_kernel)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] += tmp[i][j];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 

@@ -540,6 +540,11 @@ class _Exec:
         return Kn.bn_backward(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.part, self._coef(),
                               self.m.G(name + ".weight"), self.m.G(name + ".bias"), add1=add1, add2=add2, out=out)
 
+    def bn_bwd_split(self, name, dz, x, relu):
+        sc, sh, mu, istd = self.bnc(name)
+        return Kn.bn_backward_split(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.part,
+                                    self._coef(), self.m.G(name + ".weight"), self.m.G(name + ".bias"), 3, 1)
+
     def wgrad(self, name, dy, x, KS, stride=1, pro=None):
         ps, ph = (None, None) if pro is None else pro
         Kn.conv2d_wgrad(dy, x, KS, stride, self.m.G(name + ".weight"), self.m.G(name + ".bias"), ps, ph,
@@ -566,17 +571,21 @@ class _Exec:
         c3 = self.bnc(p + ".bn3")[:2]
         self.wgrad(p + ".conv3.conv", dout, t2, 1, pro=c3)
         d = self.dgrad(p + ".conv3.conv", dout)                       # d relu(bn3(t2))
-        d = self.bn_bwd(p + ".bn3", d, t2, relu=1)                     # d t2
         ws = self.m.SW(1, p + ".conv2.conv.weight")
         xs = self.saved_split.get(p + ".conv2.conv")
-        if ws is not None and ws.npieces == 3:
-            ys = Kn.split_activation(d, 3, 1)          # shared by the weight and data gradients
-            if xs is not None and Kn.wgrad3_psa_ok(ys, xs):
-                Kn.conv2d_wgrad3_psa(ys, xs, self.m.G(p + ".conv2.conv.weight"), self.m.G(p + ".conv2.conv.bias"))
-            else:
-                self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
+        split_wgrad = (ws is not None and ws.npieces == 3 and xs is not None and t2.shape[1] % 128 == 0
+                       and xs.C % 128 == 0 and t2.shape[3] % 16 == 0)
+        if split_wgrad:
+            # d t2 only as the split operand both conv2 gradients read
+            ys = self.bn_bwd_split(p + ".bn3", d, t2, relu=1)
+            Kn.conv2d_wgrad3_psa(ys, xs, self.m.G(p + ".conv2.conv.weight"), self.m.G(p + ".conv2.conv.bias"))
             d = Kn.conv2d_forward_psa(ys, ws, None)                    # d relu(bn2(t1))
+        elif ws is not None and ws.npieces == 3:
+            d = self.bn_bwd(p + ".bn3", d, t2, relu=1)                 # d t2
+            self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
+            d = Kn.conv2d_forward_psa(Kn.split_activation(d, 3, 1), ws, None)
         else:
+            d = self.bn_bwd(p + ".bn3", d, t2, relu=1)                 # d t2
             self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
             d = self.dgrad(p + ".conv2.conv", d)                       # d relu(bn2(t1))
         d = self.bn_bwd(p + ".bn2", d, t1, relu=1)                     # d t1

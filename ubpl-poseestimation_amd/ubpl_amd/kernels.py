@@ -242,6 +242,16 @@ def bn_stats_from_partials(part, C, N, gamma, beta, eps, momentum, rmean, rvar, 
          _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift_out), stream())
 
 
+def bn_backward_split(dz, x, gamma, mean, invstd, scale, shift, relu, part, coef, dgamma, dbeta, npieces, pad):
+    """bn_backward with dx delivered as a SplitAct (PSA planes) only."""
+    B, C, H, W = x.shape
+    plane = B * C * (H + 2 * pad) * (W + 2 * pad)
+    out = torch.empty(npieces * plane, device=x.device, dtype=torch.int16)
+    call("ubpl_bn_backward_split", _p(dz), _p(x), B, C, H, W, _p(gamma), _p(mean), _p(invstd), _p(scale), _p(shift),
+         int(relu), _p(part), _p(coef), _p(dgamma), _p(dbeta), int(pad), int(npieces), _p(out), int(plane), stream())
+    return SplitAct(out, plane, B, C, H, W, pad, npieces)
+
+
 def bn_backward(dz, x, gamma, mean, invstd, scale, shift, relu, part, coef, dgamma, dbeta, add1=None, add2=None,
                 out=None):
     B, C = x.shape[:2]
