@@ -138,36 +138,42 @@ __device__ __forceinline__ float half_sum_dpp(float v) {
 // 4(l>>5)): per channel m and per 64-pixel slice q = n/64 of the flat (b, p)
 // range, part[(m*np + q)*2 + {0,1}] = (S, M2): S = sum y, M2 = sum (y - S/n)^2
 // over the slice's n valid pixels (Chan's parallel form: no E[y^2] - E[y]^2
-// cancellation; the finalize combines slices in f64).  A wave covers one slice
-// (its 64 pixels: TN = 2 fragments of 32).
+// cancellation; the finalize combines slices in f64).  A wave covers TN/2
+// slices (2 fragments of 32 pixels each).
 template <int TM, int TN, typename ACC>
 __device__ __forceinline__ void tile_bn_partials(const ACC (&acc)[TM][TN], const bool (&nok)[TN], int mrow0, int M,
                                                  int64_t nwave0, int64_t N, float* part) {
-    static_assert(TN == 2, "one wave = one 64-pixel slice");
-    if (nwave0 >= N) return;
+    static_assert(TN % 2 == 0, "a wave covers whole 64-pixel slices (2 fragments of 32 each)");
     const int lane = threadIdx.x & 63, h = lane >> 5;
     const int64_t np = (N + 63) / 64;
-    const int64_t q = nwave0 / 64;
-    const float inv_n = 1.f / (float)(N - nwave0 < 64 ? N - nwave0 : 64);
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int sp = 0; sp < TN / 2; ++sp) {
+        const int64_t ns0 = nwave0 + 64 * sp;
+        if (ns0 >= N) break;
+        const int64_t q = ns0 / 64;
+        const float inv_n = 1.f / (float)(N - ns0 < 64 ? N - ns0 : 64);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int m = mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float y0 = nok[0] ? acc[i][0][r] : 0.f;
-            const float y1 = nok[1] ? acc[i][1][r] : 0.f;
-            const float s = half_sum_dpp(y0 + y1);
-            const float s_lo = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s), 31));
-            const float s_hi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s), 63));
-            const float mu = (h ? s_hi : s_lo) * inv_n;
-            const float d0 = nok[0] ? y0 - mu : 0.f;
-            const float d1 = nok[1] ? y1 - mu : 0.f;
-            const float m2 = half_sum_dpp(fmaf(d0, d0, d1 * d1));
-            if ((lane & 31) == 31 && m < M) {
-                part[(m * np + q) * 2] = s;
-                part[(m * np + q) * 2 + 1] = m2;
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float y0 = nok[2 * sp] ? acc[i][2 * sp][r] : 0.f;
+                const float y1 = nok[2 * sp + 1] ? acc[i][2 * sp + 1][r] : 0.f;
+                const float s = half_sum_dpp(y0 + y1);
+                const float s_lo =
+                    __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s), 31));
+                const float s_hi =
+                    __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, s), 63));
+                const float mu = (h ? s_hi : s_lo) * inv_n;
+                const float d0 = nok[2 * sp] ? y0 - mu : 0.f;
+                const float d1 = nok[2 * sp + 1] ? y1 - mu : 0.f;
+                const float m2 = half_sum_dpp(fmaf(d0, d0, d1 * d1));
+                if ((lane & 31) == 31 && m < M) {
+                    part[(m * np + q) * 2] = s;
+                    part[(m * np + q) * 2 + 1] = m2;
+                }
             }
-        }
+    }
 }
 
 }  // namespace ubpl

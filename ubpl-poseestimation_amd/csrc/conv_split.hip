@@ -18,6 +18,7 @@
 // re-layout into NP bf16 planes); activations are split while they are staged,
 // after the fused BN+ReLU prologue.
 #include "common.h"
+#include <cstdlib>
 using ubpl::xcd_remap;
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -327,7 +328,7 @@ __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int KS, int NP>
+template <int BM, int KS, int NP, int BNT = 128>
 __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
@@ -335,21 +336,24 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                                                         float* __restrict__ slab, float* __restrict__ stat_part) {
     constexpr int PADK = (KS - 1) / 2;
     constexpr int T = KS * KS;
-    constexpr int TM = BM / 64, TN = BN / 64;
-    constexpr int AB = NP * BM * 32, BB = NP * BN * 32;   // bytes per stage
-    constexpr int NS = 3;
+    constexpr int TM = BM / 64, TN = BNT / 64;
+    constexpr int AB = NP * BM * 32, BB = NP * BNT * 32;   // bytes per stage
+    // 128-pixel tiles: 3-stage ring; 256-pixel tiles (wave tile 64 x 128, twice
+    // the MFMAs per barrier and per fragment byte): 2 stages, 2 workgroups per CU
+    constexpr int NS = BNT == 256 ? 2 : 3;
+    constexpr int BQ = BNT / 128;                          // B DMA instructions per wave per piece
     __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
 
     const int P = H * W, Hp = H + 2 * pad, Wp = W + 2 * pad, G = Cin >> 4;
     const int64_t N = (int64_t)B * P;
     const int Ktot = Cin * T;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
+    const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BNT / 2);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                               gridDim.x * gridDim.y * gridDim.z);
     const int by = lam % gridDim.y, bx = (lam / gridDim.y) % gridDim.x, bz = lam / (gridDim.y * gridDim.x);
     const int m0 = by * BM;
-    const int64_t n0 = (int64_t)bx * BN;
+    const int64_t n0 = (int64_t)bx * BNT;
     const int k_begin = bz * kchunk;
     const int k_end = min(Ktot, k_begin + kchunk);
 
@@ -360,14 +364,16 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
     // per-lane 32-bit byte offsets over wave-uniform bases (scalar + vector
     // addressing: no 64-bit VALU per DMA instruction)
     const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, Cout - 1) * Ktot + 8 * lchunk) * 2);
-    uint32_t b_lane;
-    {
-        int64_t n = n0 + 32 * wid + lr;
+    uint32_t b_lane[BQ];   // wave w moves pixel rows 32*(BQ*w + q) .. +31
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+        int64_t n = n0 + 32 * (BQ * wid + q) + lr;
         n = n < N ? n : N - 1;
         const int b = (int)(n / P);
         const int p = (int)(n - (int64_t)b * P);
         const int oh = p / W, ow = p - oh * W;
-        b_lane = (uint32_t)(((((int64_t)b * G * Hp + oh + pad - PADK) * Wp + ow + pad - PADK) * 16 + 8 * lchunk) * 2);
+        b_lane[q] =
+            (uint32_t)(((((int64_t)b * G * Hp + oh + pad - PADK) * Wp + ow + pad - PADK) * 16 + 8 * lchunk) * 2);
     }
     auto stage = [&](int buf, int kt) {
         const int kg = kt >> 4;
@@ -382,8 +388,11 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             if (a_issue)
                 __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane),
                                                  (lds_ptr_t)(base + p * BM * 32 + wid * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
-                                             (lds_ptr_t)(base + AB + p * BN * 32 + wid * 1024), 16, 0, 0);
+#pragma unroll
+            for (int q = 0; q < BQ; ++q)
+                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane[q]),
+                                                 (lds_ptr_t)(base + AB + p * BNT * 32 + (BQ * wid + q) * 1024), 16,
+                                                 0, 0);
         }
     };
 
@@ -419,19 +428,19 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 
     const int nkt = (k_end - k_begin) >> 4;
     if (nkt > 0) stage(0, k_begin);
-    if (nkt > 1) stage(1, k_begin + 16);
+    if (NS == 3 && nkt > 1) stage(1, k_begin + 16);
     for (int t = 0; t < nkt; ++t) {
         // retire stage t (this wave's DMA), then the barrier: every wave's
         // stage t has landed and every wave is done reading stage t-1
-        if (t + 1 < nkt) {
-            if (a_issue) vm_wait<2 * NP>();
-            else vm_wait<NP>();
+        if (NS == 3 && t + 1 < nkt) {
+            if (a_issue) vm_wait<NP + BQ * NP>();
+            else vm_wait<BQ * NP>();
         } else {
             vm_wait<0>();
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (t + 2 < nkt) stage((t + 2) % NS, k_begin + (t + 2) * 16);
+        if (t + NS - 1 < nkt) stage((t + NS - 1) % NS, k_begin + (t + NS - 1) * 16);
         const int cur = t % NS;
         const char* base = lds + cur * (AB + BB);
         bf16x8 af[TM][NP], bfr[TN][NP];
@@ -447,10 +456,22 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             const int row = wn + 32 * j + li;
 #pragma unroll
             for (int p = 0; p < NP; ++p)
-                bfr[j][p] = *reinterpret_cast<const bf16x8*>(base + AB + p * BN * 32 + row * 32 +
+                bfr[j][p] = *reinterpret_cast<const bf16x8*>(base + AB + p * BNT * 32 + row * 32 +
                                                             16 * (h ^ ((row >> 3) & 1)));
         }
-        if constexpr (NP == 3) {
+        if constexpr (NP == 3 && TN > 2) {
+            // (no register room for every tile's chunk at once)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    floatx16 tmp;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) tmp[r] = 0.f;
+                    mfma_split<NP>(tmp, af[i], bfr[j]);
+                    acc[i][j] += tmp;
+                }
+        } else if constexpr (NP == 3) {
             // every tile's chunk chain first, the f32 adds after them (behind a
             // scheduling barrier): an add right behind its own chain waits out
             // the MFMA latency (s_nop) with the other tiles' chains not issued
@@ -818,14 +839,14 @@ Plan fwd_plan(int Cout, int64_t N, int Ktot, int np, bool psa = false) {
 void launch_split_reduce(const float* slab, int splits, int Cout, int P, int64_t N, const float* bias,
                          const float* res, float* y, hipStream_t st);
 
-template <int BM, int KS, int NP>
+template <int BM, int KS, int NP, int BNT>
 int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t wplane, const float* bias,
                const float* res, float* y, int B, int Cin, int H, int W, int pad, int Cout, const Plan& pl,
                float* slab, float* stat_part, hipStream_t st) {
     const int64_t N = (int64_t)B * H * W;
-    dim3 grid((unsigned)((N + BN - 1) / BN), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
+    dim3 grid((unsigned)((N + BNT - 1) / BNT), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
     const bool split = pl.splits > 1;
-    hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP>), grid, dim3(NT), 0, st, xs, xplane, wp, wplane, bias,
+    hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT>), grid, dim3(NT), 0, st, xs, xplane, wp, wplane, bias,
                        split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr,
                        split ? nullptr : stat_part);
     UBPL_LAUNCH_CHECK();
@@ -1000,9 +1021,22 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     const int64_t N = (int64_t)B * H * W;
     const Plan pl = fwd_plan(Cout, N, Cin * KS * KS, npieces, true);
     if (pl.splits > 1 && slab == nullptr) return (int)hipErrorInvalidValue;
+    // unsplit 128-row launches run on 256-pixel tiles (+12 % on the 64x64-level
+    // 3x3 conv); tuning hook: UBPL_PSA_BN=128 keeps 128-pixel tiles everywhere
+    static const bool bn256 = [] {
+        const char* e = getenv("UBPL_PSA_BN");
+        return !(e && atoi(e) == 128);
+    }();
+    if (bn256 && pl.bm == 128 && pl.splits == 1 && npieces == 3 && N % 256 == 0) {
+        if (KS == 3)
+            return launch_psa<128, 3, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
+                                              slab, stat_part, st);
+        return launch_psa<128, 1, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
+                                          slab, stat_part, st);
+    }
 #define UBPL_PS(BM_, KS_, NP_) \
-    return launch_psa<BM_, KS_, NP_>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl, slab, \
-                                     stat_part, st)
+    return launch_psa<BM_, KS_, NP_, 128>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl, \
+                                          slab, stat_part, st)
 #define UBPL_PS_BM(KS_, NP_)          \
     if (pl.bm == 128) UBPL_PS(128, KS_, NP_); \
     UBPL_PS(64, KS_, NP_)
