@@ -195,6 +195,16 @@ int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int
 int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                             const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
                             const float* res, float* y, float* slab, int npieces, float* stat_part, void* stream);
+/* 1x1 stride-1 conv on the 6xbf16 path with the f32 activations split while
+ * they are staged (no pre-split image): y = conv(relu(x*pscale + pshift) or x)
+ * + bias (+ res, may alias y); wsplit = 3 planes of [Cout][Cin] from
+ * ubpl_conv_weights_split (KS = 1).  Cin % 16 == 0, Cout % 64 == 0, P % 4 == 0.
+ * stat_part (nullable): BatchNorm partials of y (ubpl_bn_partials layout).
+ * _preferred: 1 when the shape is supported and fills the chip. */
+int ubpl_conv1x1_split_load_preferred(int B, int Cin, int Cout, int P);
+int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int P, const uint16_t* wsplit, int64_t wplane,
+                                    const float* bias, int Cout, const float* pscale, const float* pshift,
+                                    const float* res, float* y, float* stat_part, void* stream);
 
 /* MaxPool2d(2,2) (models/base/layers.py:93), Upsample(x2, nearest) + add
  * (layers.py:110-111), AvgPool2d(2,2) projection (models/pose/hourglass.py:226). */

@@ -215,3 +215,66 @@ def test_bn_backward_split_matches_f32_then_split():
         outs.append((ys.buf.cpu(), dg.cpu(), db.cpu()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+# (B, Cin, H, Cout, prologue, residual): 128- and 64-row tiles, a pixel tail
+# (N % 256 != 0) and 256-pixel tiles spanning several images (P < 256)
+SOL_CASES = [
+    (2, 256, 64, 128, True, False),
+    (2, 128, 64, 256, True, True),
+    (3, 64, 32, 64, True, True),
+    (5, 256, 8, 256, False, True),
+    (3, 128, 6, 128, True, False),
+]
+
+
+@pytest.mark.parametrize("case", SOL_CASES)
+def test_conv1x1_split_load_vs_f64(case):
+    """conv1x1_sol_kernel: forward (prologue, residual, BN partials) and the
+    data gradient through the mode-1 table, within 2x the f32 path's error."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, H, Cout, pro, resid = case
+    gen = torch.Generator().manual_seed(5 + hash(case) % 1000)
+    x32 = torch.randn(B, Cin, H, H, generator=gen)
+    w32 = torch.randn(Cout, Cin, 1, 1, generator=gen) / np.sqrt(Cin)
+    b32 = torch.randn(Cout, generator=gen)
+    sc32 = torch.rand(Cin, generator=gen) + 0.5
+    sh32 = torch.randn(Cin, generator=gen) * 0.5
+    res32 = torch.randn(B, Cout, H, H, generator=gen) if resid else None
+    inp = F.relu(x32.double() * sc32.double()[None, :, None, None] + sh32.double()[None, :, None, None]) if pro \
+        else x32.double()
+    yref = F.conv2d(inp, w32.double(), b32.double())
+    if resid:
+        yref = yref + res32.double()
+    d = lambda t: None if t is None else t.to(DEV)
+    ps, ph = (d(sc32), d(sh32)) if pro else (None, None)
+    y_f32 = Kn.conv2d_forward(d(x32), d(w32), d(b32), 1, ps, ph, res=d(res32))
+    part = Kn.bn_partial_buffer(Cout, B * H * H, DEV)
+    y = Kn.conv1x1_forward_split_load(d(x32), Kn.conv_weight_split(d(w32), 0, 3), d(b32), ps, ph, res=d(res32),
+                                      stat_part=part)
+    e32, esp = _rel(y_f32, yref), _rel(y, yref)
+    print("sol fwd %s: f32 %.2e split-load %.2e" % (case, e32, esp))
+    assert esp <= 2 * e32 + 1e-8, (esp, e32)
+    # BN statistics from the epilogue partials
+    gamma, beta = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
+    rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    mu, istd, s_, h_ = (torch.empty(Cout, device=DEV) for _ in range(4))
+    Kn.bn_stats_from_partials(part, Cout, B * H * H, gamma, beta, 1e-5, 0.1, rm, rv, mu, istd, s_, h_)
+    yd = y.double().cpu()
+    torch.testing.assert_close(mu.double().cpu(), yd.mean((0, 2, 3)), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(istd.double().cpu(), 1.0 / torch.sqrt(yd.var((0, 2, 3), unbiased=False) + 1e-5),
+                               rtol=1e-5, atol=0)
+    # residual aliasing the output
+    if resid:
+        o = d(res32).clone()
+        Kn.conv1x1_forward_split_load(d(x32), Kn.conv_weight_split(d(w32), 0, 3), d(b32), ps, ph, res=o, out=o)
+        assert torch.equal(o, y)
+    # data gradient (x = dy, mode-1 weights [Cin][Cout]); Cin plays the output role
+    if Cin % 64 == 0:
+        dy = torch.randn(B, Cout, H, H, generator=gen)
+        dxref = torch.nn.grad.conv2d_input((B, Cin, H, H), w32.double(), dy.double())
+        dx = Kn.conv1x1_forward_split_load(d(dy), Kn.conv_weight_split(d(w32), 1, 3), None)
+        dx32 = Kn.conv2d_dgrad(d(dy), d(w32))
+        e32, esp = _rel(dx32, dxref), _rel(dx, dxref)
+        print("sol dgrad %s: f32 %.2e split-load %.2e" % (case, e32, esp))
+        assert esp <= 2 * e32 + 1e-8, (esp, e32)

@@ -20,8 +20,8 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
-    H = 64
-    for cin, cout in ((256, 128), (128, 256), (256, 256), (128, 128)):
+    H = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+    for cin, cout in ((256, 128), (128, 256), (256, 256), (128, 128), (64, 128), (128, 64)):
         x = torch.randn(B, cin, H, H, device=dev, generator=g)
         w = torch.randn(cout, cin, 1, 1, device=dev, generator=g) * 0.05
         b = torch.randn(cout, device=dev, generator=g)
@@ -43,7 +43,15 @@ def main():
             ("dma pro", lambda: Kn.conv1x1_forward_kmajor(x, wk, b, ps, ph, out=y), mb(x, y)),
             ("dma pro+res", lambda: Kn.conv1x1_forward_kmajor(x, wk, b, ps, ph, res=res, out=y), mb(x, y, res)),
         ]
+        ws = Kn.conv_weight_split(w, 0, 3)
+        cases += [
+            ("sol plain", lambda: Kn.conv1x1_forward_split_load(x, ws, b, out=y), mb(x, y)),
+            ("sol pro", lambda: Kn.conv1x1_forward_split_load(x, ws, b, ps, ph, out=y), mb(x, y)),
+            ("sol pro+res", lambda: Kn.conv1x1_forward_split_load(x, ws, b, ps, ph, res=res, out=y), mb(x, y, res)),
+        ]
+        ysl = Kn.conv1x1_forward_split_load(x, ws, b, ps, ph, res=res)
         yd = Kn.conv1x1_forward_kmajor(x, wk, b, ps, ph, res=res)
+        print("sol vs f32 rel %.2e" % float((ysl - yd).norm() / yd.norm()))
         yr = Kn.conv2d_forward(x, w, b, 1, ps, ph, res=res)
         print("dma vs f32 kernel rel %.2e" % float((yd - yr).norm() / yr.norm()))
         for name, fn, mbytes in cases:
@@ -58,6 +66,10 @@ def main():
                                                                  mb(dy, dx) / t / 1e3))
         t = timeit(lambda: Kn.conv1x1_forward_kmajor(dy, w, None, out=dx), reps)
         print("1x1 %3d->%3d %-12s %7.3f ms %6.1f TF %6.2f TB/s" % (cin, cout, "dma dgrad", t, fl / t / 1e9,
+                                                                 mb(dy, dx) / t / 1e3))
+        wsd = Kn.conv_weight_split(w, 1, 3)
+        t = timeit(lambda: Kn.conv1x1_forward_split_load(dy, wsd, None, out=dx), reps)
+        print("1x1 %3d->%3d %-12s %7.3f ms %6.1f TF %6.2f TB/s" % (cin, cout, "sol dgrad", t, fl / t / 1e9,
                                                                  mb(dy, dx) / t / 1e3))
         dw, db = torch.zeros_like(w), torch.zeros_like(b)
         t = timeit(lambda: Kn.conv2d_wgrad(dy, x, 1, 1, dw, db, ps, ph, accumulate=False), reps)

@@ -3,12 +3,12 @@
 # over tools/pmc_conv.py; each pass its own process.  Stops on the first failure.
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
-OUT=gpurun_out/pmc
+OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p $OUT
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 pass() {
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --pmc "$@" -d $OUT -o $name --output-format csv -- python3 tools/pmc_conv.py > $OUT/$name.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc "$@" -d $OUT -o $name --output-format csv -- python3 ${WORKLOAD:-tools/pmc_conv.py} > $OUT/$name.log 2>&1
   local rc=$?
   echo "pmc $name rc=$rc"
   return $rc

@@ -80,6 +80,48 @@ __device__ __forceinline__ float block_max(float v, float* smem) {
 
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// MFMA accumulators (32x32 C/D map: lane l holds pixel l&31 of rows (r&3) +
+// 8(r>>2) + 4(l>>5)) seeded with bias (+ residual) before the K loop, so the
+// epilogue only stores; an element is read and written by the same lane, so
+// res may alias the output.  The cases are wave-uniform branches; inside one,
+// loads are unconditional (clamped rows): a load under a per-lane condition
+// becomes a branch + vmcnt(0) per element.  No residual: nothing is read.
+template <int TM, int TN, typename ACC>
+__device__ __forceinline__ void seed_acc(ACC (&acc)[TM][TN], const float* bias, const float* res,
+                                         const int64_t (&obase)[TN], int mrow0, int M, int P) {
+    const int h = (threadIdx.x & 63) >> 5;
+    if (res != nullptr) {
+        const bool hb = bias != nullptr;
+        const float* bp = hb ? bias : res;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = min(mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
+                    const float bv = bp[m];
+                    acc[i][j][r] = (hb ? bv : 0.f) + res[obase[j] + (int64_t)m * P];
+                }
+    } else if (bias != nullptr) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float bv = bias[min(mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1)];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j][r] = bv;
+            }
+    } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    }
+}
+
 // Two floats -> NP packed bf16 pairs (piece p of a in the low half): the
 // split-bf16 representation v = v0 + v1 (+ v2), v_p = bf16(v - v_0 - ... - v_{p-1}).
 template <int NP>

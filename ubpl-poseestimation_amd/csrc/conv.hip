@@ -236,22 +236,9 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
         const int p = (int)(nc - (int64_t)b * P);
         obase[j] = (int64_t)b * Cout * P + p;
     }
-    // (unconditional loads from always-valid pointers, then selects: a load
-    // under a runtime condition becomes a branch + vmcnt(0) per element)
     floatx16 acc[TM][TN];
-    const bool hb = slab == nullptr && bias != nullptr, hr = slab == nullptr && res != nullptr;
-    const float* bp = bias ? bias : y;
-    const float* rp = res ? res : y;
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk, Cout - 1);
-                const float bv = bp[m], rv = rp[obase[j] + (int64_t)m * P];
-                acc[i][j][r] = (hb ? bv : 0.f) + (hr ? rv : 0.f);
-            }
+    const bool direct = slab == nullptr;
+    ubpl::seed_acc<TM, TN>(acc, direct ? bias : nullptr, direct ? res : nullptr, obase, m0 + wm, Cout, P);
 
     if (PRO) __syncthreads();  // s_sc / s_sh ready
     const int nkt = (k_end - k_begin + BK - 1) / BK;
@@ -420,22 +407,9 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_dma_kernel(const float* __restr
         const int p = (int)(nc - (int64_t)b * P);
         obase[j] = (int64_t)b * M * P + p;
     }
-    // (unconditional loads from always-valid pointers, then selects: a load
-    // under a runtime condition becomes a branch + vmcnt(0) per element)
     floatx16 acc[TM][TN];
-    const bool hb = slab == nullptr && bias != nullptr, hr = slab == nullptr && res != nullptr;
-    const float* bp = bias ? bias : y;
-    const float* rp = res ? res : y;
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk, M - 1);
-                const float bv = bp[m], rv = rp[obase[j] + (int64_t)m * P];
-                acc[i][j][r] = (hb ? bv : 0.f) + (hr ? rv : 0.f);
-            }
+    const bool direct = slab == nullptr;
+    ubpl::seed_acc<TM, TN>(acc, direct ? bias : nullptr, direct ? res : nullptr, obase, m0 + wm, M, P);
 
     const int nkt = (k_end - k_begin + BK - 1) / BK;
     if (nkt > 0) stage(0, k_begin);

@@ -409,22 +409,9 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
         const int p = (int)(nc - (int64_t)b * P);
         obase[j] = (int64_t)b * Cout * P + p;
     }
-    // (unconditional loads from always-valid pointers, then selects: a load
-    // under a runtime condition becomes a branch + vmcnt(0) per element)
     floatx16 acc[TM][TN];
-    const bool hb = slab == nullptr && bias != nullptr, hr = slab == nullptr && res != nullptr;
-    const float* bp = bias ? bias : y;
-    const float* rp = res ? res : y;
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, Cout - 1);
-                const float bv = bp[m], rv = rp[obase[j] + (int64_t)m * P];
-                acc[i][j][r] = (hb ? bv : 0.f) + (hr ? rv : 0.f);
-            }
+    const bool direct = slab == nullptr;
+    ubpl::seed_acc<TM, TN>(acc, direct ? bias : nullptr, direct ? res : nullptr, obase, m0 + wm, Cout, P);
 
     const int nkt = (k_end - k_begin) >> 4;
     if (nkt > 0) stage(0, k_begin);
@@ -525,6 +512,171 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (m < Cout) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+            }
+    }
+}
+
+// ------------------------------------------------------------------ 1x1, split on load
+// y[b,m,p] = sum_k w[m][k] v[b,k,p] + bias[m] (+ res), v = relu(x*pscale +
+// pshift) (PRO) or x, on the 6xbf16 path without a pre-split operand: the f32
+// activations (NCHW) go global -> LDS by LDS-DMA as the 16 k rows of a
+// 256-pixel tile (1 KB each; rows 8-15 shifted 128 B so the two 32-lane halves
+// of a fragment read sit in opposite bank halves), and each wave reads its own
+// pixels' B fragments from that f32 image (lane (n, h): k = 8h..8h+7 of pixel
+// n, 8 ds_read_b32), applies the prologue and splits into 3 bf16 pieces in
+// registers.  Waves split the tile along pixels (wave w: all BM rows x pixels
+// 64w..64w+63), so each value is split once per workgroup.  Weights: 3 bf16
+// planes of [M][K] (ubpl_conv_weights_split with KS = 1), staged as in
+// conv_psa_kernel.  2-stage ring, 2 workgroups per CU.  The activation read is
+// the f32 tensor itself: no split pass, no 6-byte/element PSA image.
+template <int BM, bool PRO>
+__global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restrict__ x,
+                                                           const uint16_t* __restrict__ wp, int64_t wplane,
+                                                           const float* __restrict__ bias,
+                                                           const float* __restrict__ pscale,
+                                                           const float* __restrict__ pshift, const float* res,
+                                                           float* y, int B, int K, int P, int M,
+                                                           float* __restrict__ stat_part) {
+    constexpr int NP = 3, BNT = 256, NS = 2;
+    constexpr int TM = BM / 32, TN = 2;
+    constexpr int AB = NP * BM * 32;         // A stage bytes: [piece][BM rows][32 B]
+    constexpr int BH = 8 * BNT * 4 + 128;    // one 8-row half of the B image (+ bank shift)
+    constexpr int BB = 2 * BH;
+    __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
+
+    const int64_t N = (int64_t)B * P;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wn = 64 * wid;
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    const int by = lam % gridDim.y, bx = lam / gridDim.y;
+    const int m0 = by * BM;
+    const int64_t n0 = (int64_t)bx * BNT;
+
+    // A DMA (as conv_psa_kernel): wave w < BM/32 moves rows 32w..32w+31 of each piece
+    const int lr = lane >> 1;
+    const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
+    const bool a_issue = wid < BM / 32;
+    const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, M - 1) * K + 8 * lchunk) * 2);
+    // B DMA: wave w moves k rows 4w..4w+3, lane L pixels n0 + 4L .. +3 (P % 4 == 0)
+    uint32_t b_lane;
+    {
+        int64_t n = n0 + 4 * lane;
+        n = n < N ? n : N - 4;
+        const int64_t b = n / P;
+        b_lane = (uint32_t)((b * K * P + (n - b * P)) * 4);
+    }
+    auto stage = [&](int buf, int kt) {
+        char* base = lds + buf * (AB + BB);
+        if (a_issue) {
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const char* ab = reinterpret_cast<const char*>(wp + p * wplane + kt);
+                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane),
+                                                 (lds_ptr_t)(base + p * BM * 32 + wid * 1024), 16, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = 4 * wid + q;
+            const char* bb = reinterpret_cast<const char*>(x + (int64_t)(kt + r) * P);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
+                                             (lds_ptr_t)(base + AB + (r >> 3) * BH + (r & 7) * (BNT * 4)), 16, 0, 0);
+        }
+    };
+
+    // accumulators start at bias (+ residual): see conv_psa_kernel
+    const int li = lane & 31, h = lane >> 5;
+    int64_t obase[TN];
+    bool nok[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int64_t n = n0 + wn + 32 * j + li;
+        nok[j] = n < N;
+        const int64_t nc = nok[j] ? n : N - 1;
+        const int b = (int)(nc / P);
+        const int p = (int)(nc - (int64_t)b * P);
+        obase[j] = (int64_t)b * M * P + p;
+    }
+    floatx16 acc[TM][TN];
+    ubpl::seed_acc<TM, TN>(acc, bias, res, obase, m0, M, P);
+
+    const int nkt = K >> 4;
+    stage(0, 0);
+    for (int t = 0; t < nkt; ++t) {
+        // stage t landed for every wave, every wave done with stage t-1
+        vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + 1 < nkt) stage((t + 1) & 1, (t + 1) * 16);
+        const int kt = t * 16;
+        const char* base = lds + (t & 1) * (AB + BB);
+        // this lane's k half: 8 (scale, shift) pairs (scalar loads of both halves + selects)
+        float sc[8], sh[8];
+        if (PRO) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float s0 = pscale[kt + e], s1 = pscale[kt + 8 + e];
+                const float h0 = pshift[kt + e], h1 = pshift[kt + 8 + e];
+                sc[e] = h ? s1 : s0;
+                sh[e] = h ? h1 : h0;
+            }
+        }
+        const float* bs = reinterpret_cast<const float*>(base + AB + h * BH) + wn + li;
+        bf16x8 bfr[TN][NP];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                v[e] = bs[e * BNT + 32 * j];
+                if (PRO) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
+            }
+            uint32_t pk[NP][4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                uint32_t o[NP];
+                split2<NP>(v[2 * e], v[2 * e + 1], o);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) pk[p][e] = o[p];
+            }
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const uint4 u = make_uint4(pk[p][0], pk[p][1], pk[p][2], pk[p][3]);
+                bfr[j][p] = __builtin_bit_cast(bf16x8, u);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int row = 32 * i + li;
+            bf16x8 af[NP];
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                af[p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                // per-chunk accumulation (see conv_fwd_split_kernel)
+                floatx16 tmp;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) tmp[r] = 0.f;
+                mfma_split<NP>(tmp, af, bfr[j]);
+                acc[i][j] += tmp;
+            }
+            // (register budget: one row block's A fragments live at a time)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    if (stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0, M, n0 + wn, N, stat_part);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        if (!nok[j]) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < M) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
             }
     }
 }
@@ -1051,6 +1203,55 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
 #undef UBPL_PS_BM
 #undef UBPL_PS
     return (int)hipErrorInvalidValue;
+}
+
+// ---- 1x1 with the split on load
+namespace {
+bool sol_supported(int B, int Cin, int Cout, int P) {
+    return B > 0 && P > 0 && Cin % 16 == 0 && Cin > 0 && Cout % 64 == 0 && P % 4 == 0 && (int64_t)B * P >= 4 &&
+           (int64_t)B * Cin * P * 4 < (1LL << 32) && (int64_t)Cout * Cin * 2 < (1LL << 31);
+}
+}  // namespace
+
+// 1 when ubpl_conv1x1_forward_split_load takes this shape and fills the chip
+// (>= one 256-pixel workgroup per CU); 0: use the f32 1x1 kernel (split-K plans).
+UBPL_API int ubpl_conv1x1_split_load_preferred(int B, int Cin, int Cout, int P) {
+    if (!sol_supported(B, Cin, Cout, P)) return 0;
+    const int64_t bm = Cout % 128 == 0 ? 128 : 64;
+    const int64_t wgs = (((int64_t)B * P + 255) / 256) * (Cout / bm);
+    return wgs >= occ_info().ncu ? 1 : 0;
+}
+
+// y = conv1x1(relu(x*pscale + pshift) or x) + bias (+ res, may alias y) on the
+// 6xbf16 path, x NCHW f32 split while it is staged (conv1x1_sol_kernel).
+// wsplit: 3 bf16 planes (`wplane` elements apart) of [Cout][Cin] from
+// ubpl_conv_weights_split (mode 0 of a 1x1 conv; mode 1 = its data gradient,
+// then x = dy and Cin/Cout swap).  Cin % 16 == 0, Cout % 64 == 0, P % 4 == 0,
+// x / wsplit 16-B aligned.  stat_part (nullable): BatchNorm partials of y.
+UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int P, const uint16_t* wsplit,
+                                             int64_t wplane, const float* bias, int Cout, const float* pscale,
+                                             const float* pshift, const float* res, float* y, float* stat_part,
+                                             void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (!sol_supported(B, Cin, Cout, P) || (((uintptr_t)x) & 15) || (((uintptr_t)wsplit) & 15) || (wplane % 8))
+        return (int)hipErrorInvalidValue;
+    const bool pro = pscale != nullptr;
+    const int64_t N = (int64_t)B * P;
+    const int bm = Cout % 128 == 0 ? 128 : 64;
+    dim3 grid((unsigned)((N + 255) / 256), (unsigned)(Cout / bm));
+#define UBPL_SOL(BM_, PRO_)                                                                                       \
+    hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_>), grid, dim3(NT), 0, st, x, wsplit, wplane, bias, pscale, \
+                       pshift, res, y, B, Cin, P, Cout, stat_part)
+    if (bm == 128) {
+        if (pro) UBPL_SOL(128, true);
+        else UBPL_SOL(128, false);
+    } else {
+        if (pro) UBPL_SOL(64, true);
+        else UBPL_SOL(64, false);
+    }
+#undef UBPL_SOL
+    UBPL_LAUNCH_CHECK();
+    return 0;
 }
 
 // ---- 3x3 weight gradient on the split path

@@ -220,7 +220,9 @@ class StackedHourglass(nn.Module):
         'f32'    every conv on the exact-f32 MFMA (conv.hip);
         '6xbf16' the 3x3 convs (forward and data gradient) on split-bf16 MFMA with
                  3 bf16 pieces per operand over pre-split activations (conv_split.hip
-                 PSA path, error at the f32 path's level), the rest f32;
+                 PSA path, error at the f32 path's level), the 1x1 convs whose
+                 planes fill the chip on the same arithmetic with the activations
+                 split while they are staged, the rest f32;
         '3xbf16' every conv with 16-channel contraction groups on the 2-piece
                  register-staged split kernel (faster, ~2^-16 operands: not parity-grade).
         The stem (7x7, stride 2, 3 input channels) always runs in f32."""
@@ -241,7 +243,8 @@ class StackedHourglass(nn.Module):
             for name, shape, kind, live in tab:
                 if kind != "cw" or not live or name == stem or not pieces or shape[1 if mode == 0 else 0] % 16:
                     continue
-                if pieces == 3 and shape[2] != 3:
+                # 6xbf16: 3x3 (PSA path) and 1x1 with 64-row output tiles (split on load)
+                if pieces == 3 and not (shape[2] == 3 or (shape[2] == 1 and shape[0 if mode == 0 else 1] % 64 == 0)):
                     continue
                 s, n, _ = offs[name]
                 T = shape[2] * shape[3]
@@ -253,8 +256,9 @@ class StackedHourglass(nn.Module):
         self._wlay = {}
         for mode in (0, 1):
             need = (lambda ks, nm: ks > 1) if mode == 0 else (lambda ks, nm: nm != stem)
+            # (1x1 convs stay in "rest" too: the f32 kernel takes the small planes)
             for key, keep in ((mode, need), (("rest", mode), lambda ks, nm, m=mode, f=need:
-                                               f(ks, nm) and nm not in self._wsp[m][2])):
+                                               f(ks, nm) and (ks == 1 or nm not in self._wsp[m][2]))):
                 rows, idx, o = [], {}, 0
                 for name, shape, kind, live in tab:
                     if kind != "cw" or not live or not keep(shape[2], name):
@@ -474,6 +478,11 @@ class _Exec:
         B, Cout = x.shape[0], w.shape[0]
         mkpart = lambda: Kn.bn_partial_buffer(Cout, B * x.shape[2] * x.shape[3], x.device) if stats else None
         ws = self.m.SW(0, name + ".weight") if stride == 1 else None
+        if ws is not None and ws.npieces == 3 and ws.shape[1] == 1:
+            if Kn.conv1x1_split_load_ok(x, ws):
+                part = mkpart()
+                return Kn.conv1x1_forward_split_load(x, ws, b, ps, ph, res=res, out=out, stat_part=part), part
+            ws = None                                    # small plane: the f32 1x1 kernel
         if ws is not None:
             if ws.npieces == 3:
                 part = mkpart()
@@ -552,6 +561,10 @@ class _Exec:
 
     def dgrad(self, name, dy, res=None, out=None):
         ws = self.m.SW(1, name + ".weight")
+        if ws is not None and ws.npieces == 3 and ws.shape[1] == 1:
+            if Kn.conv1x1_split_load_ok(dy, ws):
+                return Kn.conv1x1_forward_split_load(dy, ws, None, res=res, out=out)
+            ws = None
         if ws is not None:
             if ws.npieces == 3:
                 ys = Kn.split_activation(dy, 3, (ws.shape[1] == 9) * 1)

@@ -447,6 +447,30 @@ def conv2d_forward_psa(xs, ws, bias, res=None, out=None, stat_part=None):
     return y
 
 
+def conv1x1_split_load_ok(x, ws):
+    """The 6xbf16 split-on-load 1x1 kernel takes this shape and fills the chip."""
+    B, Cin, H, W = x.shape
+    return (ws is not None and ws.npieces == 3 and ws.shape[1] == 1 and ws.shape[2] == Cin
+            and x.data_ptr() % 16 == 0
+            and bool(_lib.lib().ubpl_conv1x1_split_load_preferred(B, Cin, ws.shape[0], H * W)))
+
+
+def conv1x1_forward_split_load(x, ws, bias, pscale=None, pshift=None, res=None, out=None, stat_part=None):
+    """1x1 stride-1 conv on the 6xbf16 path with x (NCHW f32) split while it is
+    staged: y = conv(relu(x*pscale + pshift) or x, ws) + bias (+ res; res may
+    alias out); ws = SplitWeights (rows, 1, Cin) — a forward (mode 0) or a data
+    gradient (mode 1, x = dy) table; stat_part: BatchNorm partials of y."""
+    B, Cin, H, W = x.shape
+    Cout, T, wc = ws.shape
+    if T != 1 or wc != Cin or ws.npieces != 3:
+        raise AssertionError("split-load 1x1: weights {} / pieces {} for {} input channels".format(
+            ws.shape, ws.npieces, Cin))
+    y = torch.empty((B, Cout, H, W), device=x.device, dtype=F32) if out is None else out
+    call("ubpl_conv1x1_forward_split_load", _p(x), B, Cin, H * W, ws.ptr(), int(ws.plane), _p(bias), Cout,
+         _p(pscale), _p(pshift), _p(res), _p(y), _p(stat_part), stream())
+    return y
+
+
 def wgrad3_psa_ok(ys, xs):
     return (ys.npieces == 3 and xs.npieces == 3 and ys.pad == 1 and xs.pad == 1 and xs.C % 128 == 0
             and ys.C % 128 == 0 and xs.W % 16 == 0 and (ys.B, ys.H, ys.W) == (xs.B, xs.H, xs.W))
