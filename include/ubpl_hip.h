@@ -218,6 +218,11 @@ int ubpl_upsample2x_add_forward(const float* up, const float* low, int64_t plane
 int ubpl_upsample2x_add_backward(const float* dout, int64_t planes, int H, int W, float* dlow, int accumulate,
                                  void* stream);
 int ubpl_add(const float* a, const float* b, int64_t n, float* out, void* stream);
+/* The same forwards + BatchNorm partials of the output for the BN that
+ * consumes it (ubpl_bn_partials layout); output planes of a multiple of 64 pixels. */
+int ubpl_maxpool2x2_forward_stats(const float* x, int B, int C, int H, int W, float* y, float* part, void* stream);
+int ubpl_upsample2x_add_forward_stats(const float* up, const float* low, int B, int C, int H, int W, float* out,
+                                      float* part, void* stream);
 
 #ifdef __cplusplus
 }

@@ -420,3 +420,32 @@ def test_conv_epilogue_bn_partials(case):
     _close(mu, m_ref, rtol=1e-6, atol=1e-6)
     _close(istd, 1.0 / torch.sqrt(v_ref + 1e-5), rtol=1e-5, atol=0)
     _close(rv, 0.9 + 0.1 * yd.var((0, 2, 3), unbiased=True), rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("kind", ["maxpool", "upsample"])
+@pytest.mark.parametrize("shape", [(4, 128, 16, 16), (3, 64, 32, 32), (2, 256, 8, 8)])
+def test_pool_stats_partials(kind, shape):
+    """The max-pool / upsample-add outputs are bit-identical with and without
+    the BatchNorm partials, and the statistics from those partials equal the
+    output's own (the residual bn1 that reads them, hourglass.py residual)."""
+    from ubpl_amd import kernels as Kn
+    B, C, H, W = shape
+    gen = torch.Generator().manual_seed(3)
+    x = (torch.randn(B, C, 2 * H, 2 * W, generator=gen) * 2 + 1).to(DEV)
+    up = (torch.randn(B, C, H, W, generator=gen) + 3).to(DEV)
+    low = torch.randn(B, C, H // 2, W // 2, generator=gen).to(DEV)
+    part = Kn.bn_partial_buffer(C, B * H * W, DEV)
+    if kind == "maxpool":
+        y0 = Kn.maxpool2x2(x)
+        y = Kn.maxpool2x2(x, stat_part=part)
+    else:
+        y0 = Kn.upsample2x_add(up, low)
+        y = Kn.upsample2x_add(up.clone(), low, stat_part=part)
+    assert torch.equal(y, y0)
+    gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    mu, istd, sc, sh = (torch.empty(C, device=DEV) for _ in range(4))
+    Kn.bn_stats_from_partials(part, C, B * H * W, gamma, beta, 1e-5, 0.1, rm, rv, mu, istd, sc, sh)
+    yd = y.double().cpu()
+    _close(mu, yd.mean((0, 2, 3)), rtol=1e-6, atol=1e-6)
+    _close(istd, 1.0 / torch.sqrt(yd.var((0, 2, 3), unbiased=False) + 1e-5), rtol=1e-5, atol=0)

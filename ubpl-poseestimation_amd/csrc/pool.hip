@@ -15,9 +15,27 @@ int grid_ew(int64_t n) {
     return (int)g;
 }
 
+// BatchNorm partials of an output written in NCHW order by one element per
+// lane, Ho*Wo % 64 == 0: the 64 outputs of a wave are one 64-pixel slice of
+// one channel (the conv epilogue's layout, common.h tile_bn_partials): S and
+// M2 about the slice mean.  i0 = the wave's first flat index.
+__device__ __forceinline__ void wave_bn_partial(float v, int64_t i0, int C, int P, int64_t np, float* part) {
+    const float s = ubpl::wave_sum(v);
+    const float d = v - s * (1.f / 64.f);
+    const float m2 = ubpl::wave_sum(d * d);
+    if ((threadIdx.x & 63) == 0) {
+        const int64_t bc = i0 / P;
+        const int c = (int)(bc % C);
+        const int64_t q = ((bc / C) * P + (i0 - bc * P)) >> 6;
+        part[((int64_t)c * np + q) * 2] = s;
+        part[((int64_t)c * np + q) * 2 + 1] = m2;
+    }
+}
+
 // planes = B*C; output Ho x Wo with Ho = H/2, Wo = W/2 (floor).
+template <bool STATS>
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const float* __restrict__ x, int64_t planes, int H, int W,
-                                                         float* __restrict__ y) {
+                                                         float* __restrict__ y, int C, float* __restrict__ part) {
     const int Ho = H >> 1, Wo = W >> 1;
     const int64_t total = planes * Ho * Wo;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -35,6 +53,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const float* __restric
         v = p[W + 1];
         if (v > m || isnan(v)) m = v;
         y[i] = m;
+        if (STATS) wave_bn_partial(m, i - (threadIdx.x & 63), C, Ho * Wo, planes / C * Ho * Wo / 64, part);
     }
 }
 
@@ -110,8 +129,10 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const float* __restric
 }
 
 // out[b,c,h,w] = up[b,c,h,w] + low[b,c,h/2,w/2]   (out may alias up)
+template <bool STATS>
 __global__ void __launch_bounds__(256) upadd_fwd_kernel(const float* up, const float* __restrict__ low,
-                                                       int64_t planes, int H, int W, float* out) {
+                                                       int64_t planes, int H, int W, float* out, int C,
+                                                       float* __restrict__ part) {
     const int Hl = H >> 1, Wl = W >> 1;
     const int64_t total = planes * H * W;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -120,7 +141,9 @@ __global__ void __launch_bounds__(256) upadd_fwd_kernel(const float* up, const f
         const int64_t t = i / W;
         const int h = (int)(t % H);
         const int64_t pl = t / H;
-        out[i] = up[i] + low[(pl * Hl + (h >> 1)) * Wl + (w >> 1)];
+        const float v = up[i] + low[(pl * Hl + (h >> 1)) * Wl + (w >> 1)];
+        out[i] = v;
+        if (STATS) wave_bn_partial(v, i - (threadIdx.x & 63), C, H * W, planes / C * H * W / 64, part);
     }
 }
 
@@ -151,7 +174,22 @@ __global__ void __launch_bounds__(256) add_kernel(const float* a, const float* b
 UBPL_API int ubpl_maxpool2x2_forward(const float* x, int64_t planes, int H, int W, float* y, void* stream) {
     const int64_t n = planes * (H / 2) * (W / 2);
     if (n == 0) return 0;
-    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, x, planes, H, W, y);
+    hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, x, planes, H,
+                       W, y, 1, nullptr);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// + BatchNorm partials of y for the BN that consumes it (ubpl_bn_partials
+// layout; N = B*(H/2)*(W/2)).  Needs (H/2)*(W/2) % 64 == 0.
+UBPL_API int ubpl_maxpool2x2_forward_stats(const float* x, int B, int C, int H, int W, float* y, float* part,
+                                           void* stream) {
+    const int64_t planes = (int64_t)B * C;
+    if (((H / 2) * (W / 2)) % 64 != 0 || part == nullptr) return (int)hipErrorInvalidValue;
+    const int64_t n = planes * (H / 2) * (W / 2);
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, x, planes, H,
+                       W, y, C, part);
     UBPL_LAUNCH_CHECK();
     return 0;
 }
@@ -188,8 +226,21 @@ UBPL_API int ubpl_upsample2x_add_forward(const float* up, const float* low, int6
                                          void* stream) {
     const int64_t n = planes * H * W;
     if (n == 0) return 0;
-    hipLaunchKernelGGL(upadd_fwd_kernel, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, up, low, planes, H, W,
-                       out);
+    hipLaunchKernelGGL(upadd_fwd_kernel<false>, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, up, low, planes,
+                       H, W, out, 1, nullptr);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// + BatchNorm partials of out (ubpl_bn_partials layout; N = B*H*W).  H*W % 64 == 0.
+UBPL_API int ubpl_upsample2x_add_forward_stats(const float* up, const float* low, int B, int C, int H, int W,
+                                               float* out, float* part, void* stream) {
+    const int64_t planes = (int64_t)B * C;
+    if ((H * W) % 64 != 0 || part == nullptr) return (int)hipErrorInvalidValue;
+    const int64_t n = planes * H * W;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(upadd_fwd_kernel<true>, dim3(grid_ew(n)), dim3(256), 0, (hipStream_t)stream, up, low, planes,
+                       H, W, out, C, part);
     UBPL_LAUNCH_CHECK();
     return 0;
 }

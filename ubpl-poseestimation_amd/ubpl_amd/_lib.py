@@ -63,6 +63,8 @@ SIGNATURES = {
     "ubpl_avgpool2x2_forward": (I, [P, L, I, I, P, P]),
     "ubpl_avgpool2x2_backward": (I, [P, L, I, I, P, I, P]),
     "ubpl_upsample2x_add_forward": (I, [P, P, L, I, I, P, P]),
+    "ubpl_maxpool2x2_forward_stats": (I, [P, I, I, I, I, P, P, P]),
+    "ubpl_upsample2x_add_forward_stats": (I, [P, P, I, I, I, I, P, P, P]),
     "ubpl_upsample2x_add_backward": (I, [P, L, I, I, P, I, P]),
     "ubpl_add": (I, [P, P, L, P, P]),
 }

@@ -19,6 +19,7 @@ models/__init__.py:4):
   autograd sees the whole network as one Function.
 """
 import math
+import os
 
 import torch
 from torch import nn
@@ -28,6 +29,9 @@ from . import kernels as Kn
 
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+# residual bn1 statistics from the producer's partials (conv epilogue, max-pool,
+# upsample-add) instead of a pass over the input; UBPL_PRODUCER_STATS=0: the pass
+_PRODUCER_STATS = os.environ.get("UBPL_PRODUCER_STATS", "1") != "0"
 
 
 # ---------------------------------------------------------------------------
@@ -363,7 +367,9 @@ class StackedHourglass(nn.Module):
         x = ex.stem(imgs)
         x = ex.residual("pre.1", x)
         x1 = x
-        x = Kn.maxpool2x2(x1)
+        part = ex.stat_buffer((x1.shape[0], x1.shape[1], x1.shape[2] // 2, x1.shape[3] // 2))
+        x = Kn.maxpool2x2(x1, stat_part=part)
+        ex.give_part(x, part)
         ex.save("pre.2", x1)
         x = ex.residual("pre.3", x)
         x = ex.residual("pre.4", x)
@@ -378,7 +384,8 @@ class StackedHourglass(nn.Module):
             preds.append(pr)
             if i < self.nStack - 1:
                 t = ex.conv("merge_preds.%d.conv.conv" % i, pr, res=x)
-                x = ex.conv("merge_features.%d.conv.conv" % i, f, res=t, out=t)
+                x, part = ex.conv("merge_features.%d.conv.conv" % i, f, res=t, out=t, stats=True)
+                ex.give_part(x, part)
             ex.save("stack.%d" % i, (f, pr))
         P = torch.stack(preds, 1)
         Fs = torch.stack(feats, 1) if feats else None
@@ -425,6 +432,7 @@ class _Exec:
         self.m, self.B, self.dev, self.part, self.train, self.do_save = model, B, dev, part, train, save
         self.saved = {}
         self.saved_split = {}
+        self._rp = None     # (tensor, BN partials of it) from its producer, for the next residual's bn1
         C = sum(self.m._offs[b + ".weight"][1] for b in self.m._bn_names)
         self.coef = torch.empty(4 * C, device=dev)     # per BN: scale|shift|mean|invstd
         self.cidx, o = {}, 0
@@ -437,6 +445,22 @@ class _Exec:
     def save(self, key, val):
         if self.do_save:
             self.saved[key] = val
+
+    def give_part(self, y, part):
+        """y's producer wrote its BatchNorm partials: the residual that takes y
+        next reads its bn1 statistics from them (no pass over y)."""
+        self._rp = (y, part) if part is not None and _PRODUCER_STATS else None
+
+    def take_part(self, x):
+        rp, self._rp = self._rp, None
+        return rp[1] if rp is not None and rp[0] is x else None
+
+    def stat_buffer(self, x_shape):
+        """Partials buffer for an elementwise producer's output (None: not on this path)."""
+        B, C, H, W = x_shape
+        if not self.train or not _PRODUCER_STATS or not Kn.stats_ok(H, W):
+            return None
+        return Kn.bn_partial_buffer(C, B * H * W, self.dev)
 
     def bnc(self, bn):
         o, c = self.cidx[bn]
@@ -507,8 +531,8 @@ class _Exec:
         return x0
 
     def conv_bn_relu(self, p, x):
-        y = self.conv(p + ".conv", x)
-        sc, sh = self.bn(p + ".bn", y)
+        y, part = self.conv(p + ".conv", x, stats=True)
+        sc, sh = self.bn(p + ".bn", y, part)
         f = Kn.bn_apply(y, sc, sh, relu=1)
         self.save(p, (x, y))
         return f
@@ -517,28 +541,34 @@ class _Exec:
         """models/base/layers.py:69-84 (pre-activation bottleneck)."""
         cin = x.shape[1]
         cout = self.m._offs[p + ".conv3.conv.weight"][2][0]
-        c1 = self.bn(p + ".bn1", x)
+        c1 = self.bn(p + ".bn1", x, self.take_part(x))
         t1, part = self.conv(p + ".conv1.conv", x, pro=c1, stats=True)
         c2 = self.bn(p + ".bn2", t1, part)
         t2, part = self.conv(p + ".conv2.conv", t1, pro=c2, stats=True)
         c3 = self.bn(p + ".bn3", t2, part)
         if cin != cout:
             r = self.conv(p + ".skip_layer.conv", x)
-            out = self.conv(p + ".conv3.conv", t2, pro=c3, res=r, out=r)
+            out, part = self.conv(p + ".conv3.conv", t2, pro=c3, res=r, out=r, stats=True)
         else:
-            out = self.conv(p + ".conv3.conv", t2, pro=c3, res=x)
+            out, part = self.conv(p + ".conv3.conv", t2, pro=c3, res=x, stats=True)
         self.save(p, (x, t1, t2))
+        self.give_part(out, part)
         return out
 
     def hourglass(self, p, n, x):
         """models/base/layers.py:104-111."""
         up1 = self.residual(p + ".up1", x)
-        pl = Kn.maxpool2x2(x)
+        part = self.stat_buffer((x.shape[0], x.shape[1], x.shape[2] // 2, x.shape[3] // 2))
+        pl = Kn.maxpool2x2(x, stat_part=part)
+        self.give_part(pl, part)
         low1 = self.residual(p + ".low1", pl)
         low2 = self.hourglass(p + ".low2", n - 1, low1) if n > 1 else self.residual(p + ".low2", low1)
         low3 = self.residual(p + ".low3", low2)
         self.save(p, x)
-        return Kn.upsample2x_add(up1, low3, out=up1)
+        part = self.stat_buffer(up1.shape)
+        out = Kn.upsample2x_add(up1, low3, out=up1, stat_part=part)
+        self.give_part(out, part)
+        return out
 
     # ---- backward
     def _coef(self):

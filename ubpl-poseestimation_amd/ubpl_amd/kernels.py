@@ -492,11 +492,21 @@ def conv2d_dgrad(dy, w, res=None, out=None, wt=None):
 
 
 # ------------------------------------------------------------------ pool / upsample
-def maxpool2x2(x, out=None):
+def maxpool2x2(x, out=None, stat_part=None):
+    """stat_part: BatchNorm partials of the output (bn_partial_buffer; needs
+    (H/2)*(W/2) % 64 == 0, see stats_ok)."""
     B, C, H, W = x.shape
     y = torch.empty((B, C, H // 2, W // 2), device=x.device, dtype=F32) if out is None else out
-    call("ubpl_maxpool2x2_forward", _p(x), B * C, H, W, _p(y), stream())
+    if stat_part is not None:
+        call("ubpl_maxpool2x2_forward_stats", _p(x), B, C, H, W, _p(y), _p(stat_part), stream())
+    else:
+        call("ubpl_maxpool2x2_forward", _p(x), B * C, H, W, _p(y), stream())
     return y
+
+
+def stats_ok(H, W):
+    """Elementwise producers (max-pool, upsample-add) emit BatchNorm partials for planes of 64k pixels."""
+    return (H * W) % 64 == 0
 
 
 def maxpool2x2_backward(x, dy, dx, accumulate):
@@ -518,10 +528,14 @@ def avgpool2x2_backward(dy, dx, accumulate):
     return dx
 
 
-def upsample2x_add(up, low, out=None):
+def upsample2x_add(up, low, out=None, stat_part=None):
+    """stat_part: BatchNorm partials of the output (H*W % 64 == 0)."""
     B, C, H, W = up.shape
     y = torch.empty_like(up) if out is None else out
-    call("ubpl_upsample2x_add_forward", _p(up), _p(low), B * C, H, W, _p(y), stream())
+    if stat_part is not None:
+        call("ubpl_upsample2x_add_forward_stats", _p(up), _p(low), B, C, H, W, _p(y), _p(stat_part), stream())
+    else:
+        call("ubpl_upsample2x_add_forward", _p(up), _p(low), B * C, H, W, _p(y), stream())
     return y
 
 
