@@ -328,7 +328,7 @@ __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int KS, int NP, int BNT = 128>
+template <int BM, int KS, int NP, int BNT = 128, int WGM = 2>
 __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
@@ -336,7 +336,10 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                                                         float* __restrict__ slab, float* __restrict__ stat_part) {
     constexpr int PADK = (KS - 1) / 2;
     constexpr int T = KS * KS;
-    constexpr int TM = BM / 64, TN = BNT / 64;
+    // waves: WGM along the output channels x 4/WGM along the pixels (64-row
+    // tiles on 256 pixels: 1 x 4, wave tile 64 x 64)
+    constexpr int WGN = 4 / WGM;
+    constexpr int TM = BM / WGM / 32, TN = BNT / WGN / 32;
     constexpr int AB = NP * BM * 32, BB = NP * BNT * 32;   // bytes per stage
     // 128-pixel tiles: 3-stage ring; 256-pixel tiles (wave tile 64 x 128, twice
     // the MFMAs per barrier and per fragment byte): 2 stages, 2 workgroups per CU
@@ -348,7 +351,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
     const int64_t N = (int64_t)B * P;
     const int Ktot = Cin * T;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BNT / 2);
+    const int wm = (wid / WGN) * (BM / WGM), wn = (wid % WGN) * (BNT / WGN);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                               gridDim.x * gridDim.y * gridDim.z);
     const int by = lam % gridDim.y, bx = (lam / gridDim.y) % gridDim.x, bz = lam / (gridDim.y * gridDim.x);
@@ -991,14 +994,14 @@ Plan fwd_plan(int Cout, int64_t N, int Ktot, int np, bool psa = false) {
 void launch_split_reduce(const float* slab, int splits, int Cout, int P, int64_t N, const float* bias,
                          const float* res, float* y, hipStream_t st);
 
-template <int BM, int KS, int NP, int BNT>
+template <int BM, int KS, int NP, int BNT, int WGM = 2>
 int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t wplane, const float* bias,
                const float* res, float* y, int B, int Cin, int H, int W, int pad, int Cout, const Plan& pl,
                float* slab, float* stat_part, hipStream_t st) {
     const int64_t N = (int64_t)B * H * W;
     dim3 grid((unsigned)((N + BNT - 1) / BNT), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
     const bool split = pl.splits > 1;
-    hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT>), grid, dim3(NT), 0, st, xs, xplane, wp, wplane, bias,
+    hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM>), grid, dim3(NT), 0, st, xs, xplane, wp, wplane, bias,
                        split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr,
                        split ? nullptr : stat_part);
     UBPL_LAUNCH_CHECK();
@@ -1179,6 +1182,16 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         const char* e = getenv("UBPL_PSA_BN");
         return !(e && atoi(e) == 128);
     }();
+    // unsplit 64-row 3x3 launches run on 256-pixel tiles with a 1 x 4 wave
+    // layout (wave tile 64 x 64: +14-19 % on the 128x128 64-channel and the
+    // 32x32 128-channel convs); UBPL_PSA_BM64W=0 keeps 64 x 128 tiles
+    static const bool bm64w = [] {
+        const char* e = getenv("UBPL_PSA_BM64W");
+        return !(e && atoi(e) == 0);
+    }();
+    if (bm64w && pl.bm == 64 && pl.splits == 1 && npieces == 3 && KS == 3 && N % 256 == 0)
+        return launch_psa<64, 3, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
+                                            slab, stat_part, st);
     if (bn256 && pl.bm == 128 && pl.splits == 1 && npieces == 3 && N % 256 == 0) {
         if (KS == 3)
             return launch_psa<128, 3, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,

@@ -691,7 +691,7 @@ class _Exec:
         d = self.residual_bwd("pre.4", dxn)
         d = self.residual_bwd("pre.3", d)
         x1 = self.saved.get("pre.2")
-        dx1 = torch.zeros_like(x1)
+        dx1 = torch.empty_like(x1)                       # (even H, W: every element written)
         Kn.maxpool2x2_backward(x1, d, dx1, accumulate=False)
         d = self.residual_bwd("pre.1", dx1)
         imgs, y0 = self.saved.get("pre.0")
