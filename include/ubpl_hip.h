@@ -187,7 +187,7 @@ int ubpl_split_activation(const float* x, int B, int C, int H, int W, const floa
 int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int KS, int H, int W, int npieces);
 /* 3x3 weight gradient (+ bias gradient, db nullable) on the split path from PSA
  * operands with a 1-pixel border: dys = split(dy), xs = split(conv input),
- * npieces = 3; Cin % 128 == 0, Cout % 128 == 0, W % 16 == 0. */
+ * npieces = 3; Cin % 64 == 0, Cout % 64 == 0, W % 16 == 0. */
 int64_t ubpl_wgrad3_psa_workspace(int B, int Cin, int Cout, int H, int W);
 int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int Cin,
                     int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,

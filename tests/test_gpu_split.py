@@ -162,7 +162,8 @@ def test_split_activation_layout():
 
 
 @pytest.mark.parametrize("case", [(2, 128, 128, 64, 64), (3, 128, 128, 16, 32), (2, 256, 128, 32, 16),
-                                  (2, 128, 256, 16, 16)])
+                                  (2, 128, 256, 16, 16), (2, 64, 64, 32, 32), (2, 64, 128, 16, 16),
+                                  (3, 128, 64, 16, 32)])
 def test_wgrad3_psa_vs_f64(case):
     """3x3 weight + bias gradient from PSA operands (transposed LDS reads,
     split-K slab) within 2x the exact-f32 kernel's error against float64."""

@@ -700,13 +700,17 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
 // image [piece][16-channel group][16 pixel rows][32 B]; odd groups store
 // pixel rows 0-3 <-> 4-7 swapped (pre-permuted DMA source) so the two groups a
 // 32-lane half reads sit in opposite 128-B bank halves.
-template <int NP>
+template <int NP, int CB = 128>
 __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __restrict__ dys, int64_t dplane,
                                                           const uint16_t* __restrict__ xs, int64_t xplane, int B,
                                                           int Cin, int Cout, int H, int W, int steps_per_split,
                                                           float* __restrict__ slab) {
-    constexpr int BM = 128, TM = 2, TN = 2, NS = 3;
-    constexpr int AB = NP * 8 * 512, BB = NP * 8 * 512;   // bytes per stage: 8 groups x 16 px x 32 B per piece
+    // CB = channel block of both tile sides (128, or 64 for the 64-channel convs:
+    // wave tile 32 x 32, waves 0-1 move the operands)
+    constexpr int BM = CB, TM = CB / 64, TN = CB / 64, NS = 3;
+    constexpr int GR = CB / 16;                            // channel groups per operand tile
+    constexpr int PI = GR * 512;                           // piece image: GR groups x 16 px x 32 B
+    constexpr int AB = NP * PI, BB = NP * PI;              // bytes per stage
     __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
     typedef short v4i16 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) v4i16* tr_ptr_t;
@@ -715,14 +719,14 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
     const int Gci = Cin >> 4, Gco = Cout >> 4;
     const int Ntot = 9 * Cin, Nt = Ntot + 1;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+    const int wm = (wid >> 1) * (CB / 2), wn = (wid & 1) * (CB / 2);
     // tile order: n tiles (tap, ci) fastest so the 9 taps of one K split share an L2
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                               gridDim.x * gridDim.y * gridDim.z);
     const int bx = lam % gridDim.x, by = (lam / gridDim.x) % gridDim.y, bz = lam / (gridDim.x * gridDim.y);
     const int m0 = by * BM;
-    const int ntile_per_tap = Cin / 128;
-    const int tap = bx / ntile_per_tap, ci0 = (bx - tap * ntile_per_tap) * 128;
+    const int ntile_per_tap = Cin / CB;
+    const int tap = bx / ntile_per_tap, ci0 = (bx - tap * ntile_per_tap) * CB;
     const int kh = tap / 3, kw = tap - 3 * (tap / 3);
     const int wsteps = W >> 4;
     const int total_steps = B * H * wsteps;
@@ -730,7 +734,8 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
     const int s_end = min(total_steps, s_begin + steps_per_split);
     const int nkt = max(0, s_end - s_begin);
 
-    // DMA lane geometry: wave w moves channel groups 2w, 2w+1 of both operands
+    // DMA lane geometry: wave w < GR/2 moves channel groups 2w, 2w+1 of both operands
+    const bool d_issue = wid < GR / 2;
     const int gl = 2 * wid + (lane >> 5);
     const int rphys = (lane & 31) >> 1;
     const int rlog = rphys ^ (4 * (gl & 1));
@@ -748,14 +753,15 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
         const int64_t aoff = (int64_t)b * Gco * HWp * 16 + ((int64_t)(oh + 1) * Wp + ow0 + 1) * 16;
         const int64_t boff = (int64_t)b * Gci * HWp * 16 + ((int64_t)(oh + kh) * Wp + ow0 + kw) * 16;
         char* base = lds + buf * (AB + BB);
+        if (!d_issue) return;
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
             const char* ab = dys_m + 2 * (p * dplane + aoff);
             const char* bb = xs_c + 2 * (p * xplane + boff);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane), (lds_ptr_t)(base + p * 4096 + wid * 1024), 16,
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane), (lds_ptr_t)(base + p * PI + wid * 1024), 16,
                                              0, 0);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
-                                             (lds_ptr_t)(base + AB + p * 4096 + wid * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane), (lds_ptr_t)(base + AB + p * PI + wid * 1024),
+                                             16, 0, 0);
         }
     };
 
@@ -803,17 +809,17 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
         for (int p = 0; p < NP; ++p) {
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * 4096 + aoffs[i][0]));
-                const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * 4096 + aoffs[i][1]));
+                const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * PI + aoffs[i][0]));
+                const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * PI + aoffs[i][1]));
                 const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                 af[i][p] = __builtin_bit_cast(bf16x8, v);
             }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const v4i16 lo =
-                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * 4096 + boffs[j][0]));
+                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * PI + boffs[j][0]));
                 const v4i16 hi =
-                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * 4096 + boffs[j][1]));
+                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * PI + boffs[j][1]));
                 const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                 bfr[j][p] = __builtin_bit_cast(bf16x8, v);
             }
@@ -1269,8 +1275,11 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
 
 // ---- 3x3 weight gradient on the split path
 namespace {
+int wgrad3_cb(int Cin, int Cout) { return (Cin % 128 == 0 && Cout % 128 == 0) ? 128 : 64; }
+
 int wgrad3_splits(int B, int Cin, int Cout, int H, int W) {
-    const int tiles = 9 * (Cin / 128) * (Cout / 128);
+    const int cb = wgrad3_cb(Cin, Cout);
+    const int tiles = 9 * (Cin / cb) * (Cout / cb);
     const int steps = B * H * (W / 16);
     int s = 512 / tiles;                               // one round of 2 workgroups per CU, not one over
     if (s < 1) s = 1;
@@ -1281,26 +1290,32 @@ int wgrad3_splits(int B, int Cin, int Cout, int H, int W) {
 }  // namespace
 
 UBPL_API int64_t ubpl_wgrad3_psa_workspace(int B, int Cin, int Cout, int H, int W) {
-    if (Cin % 128 || Cout % 128 || W % 16) return 0;
+    if (Cin % 64 || Cout % 64 || W % 16) return 0;
     return (int64_t)wgrad3_splits(B, Cin, Cout, H, W) * Cout * (9 * Cin + 1);
 }
 
 // dw[Cout,Cin,3,3] (+)= 3x3 weight gradient, db[Cout] (+)= sum dy (nullable), from
 // PSA operands with a 1-pixel border: dys = split(dy) [B][Cout/16][H+2][W+2][16],
 // xs = split(conv input) [B][Cin/16][H+2][W+2][16], npieces = 3.  Needs
-// Cin % 128 == 0, Cout % 128 == 0, W % 16 == 0.  slab: ubpl_wgrad3_psa_workspace floats.
+// Cin % 64 == 0, Cout % 64 == 0 (128-channel tiles when both are multiples of 128), W % 16 == 0.
+// slab: ubpl_wgrad3_psa_workspace floats.
 UBPL_API int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int Cin,
                              int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,
                              void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    if (Cin % 128 || Cout % 128 || W % 16 || npieces != 3 || slab == nullptr) return (int)hipErrorInvalidValue;
+    if (Cin % 64 || Cout % 64 || W % 16 || npieces != 3 || slab == nullptr) return (int)hipErrorInvalidValue;
     if ((((uintptr_t)dys) & 15) || (((uintptr_t)xs) & 15) || (dplane % 8) || (xplane % 8)) return (int)hipErrorInvalidValue;
     const int splits = wgrad3_splits(B, Cin, Cout, H, W);
     const int steps = B * H * (W / 16);
     const int per = (steps + splits - 1) / splits;
-    dim3 grid((unsigned)(9 * (Cin / 128)), (unsigned)(Cout / 128), (unsigned)splits);
-    hipLaunchKernelGGL((wgrad3_psa_kernel<3>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout, H, W, per,
-                       slab);
+    const int cb = wgrad3_cb(Cin, Cout);
+    dim3 grid((unsigned)(9 * (Cin / cb)), (unsigned)(Cout / cb), (unsigned)splits);
+    if (cb == 128)
+        hipLaunchKernelGGL((wgrad3_psa_kernel<3, 128>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout,
+                           H, W, per, slab);
+    else
+        hipLaunchKernelGGL((wgrad3_psa_kernel<3, 64>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout,
+                           H, W, per, slab);
     UBPL_LAUNCH_CHECK();
     return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 9, db != nullptr, dw, db, accumulate, stream);
 }

@@ -32,6 +32,8 @@ BN_MOMENTUM = 0.1
 # residual bn1 statistics from the producer's partials (conv epilogue, max-pool,
 # upsample-add) instead of a pass over the input; UBPL_PRODUCER_STATS=0: the pass
 _PRODUCER_STATS = os.environ.get("UBPL_PRODUCER_STATS", "1") != "0"
+# 64-channel 3x3 weight gradients on the split path (UBPL_WGRAD3_64=0: exact-f32 kernel)
+_WGRAD3_64 = os.environ.get("UBPL_WGRAD3_64", "1") != "0"
 
 
 # ---------------------------------------------------------------------------
@@ -616,8 +618,9 @@ class _Exec:
         d = self.dgrad(p + ".conv3.conv", dout)                       # d relu(bn3(t2))
         ws = self.m.SW(1, p + ".conv2.conv.weight")
         xs = self.saved_split.get(p + ".conv2.conv")
-        split_wgrad = (ws is not None and ws.npieces == 3 and xs is not None and t2.shape[1] % 128 == 0
-                       and xs.C % 128 == 0 and t2.shape[3] % 16 == 0)
+        cb = 64 if _WGRAD3_64 else 128
+        split_wgrad = (ws is not None and ws.npieces == 3 and xs is not None and t2.shape[1] % cb == 0
+                       and xs.C % cb == 0 and t2.shape[3] % 16 == 0)
         if split_wgrad:
             # d t2 only as the split operand both conv2 gradients read
             ys = self.bn_bwd_split(p + ".bn3", d, t2, relu=1)

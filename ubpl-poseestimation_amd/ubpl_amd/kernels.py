@@ -472,8 +472,8 @@ def conv1x1_forward_split_load(x, ws, bias, pscale=None, pshift=None, res=None, 
 
 
 def wgrad3_psa_ok(ys, xs):
-    return (ys.npieces == 3 and xs.npieces == 3 and ys.pad == 1 and xs.pad == 1 and xs.C % 128 == 0
-            and ys.C % 128 == 0 and xs.W % 16 == 0 and (ys.B, ys.H, ys.W) == (xs.B, xs.H, xs.W))
+    return (ys.npieces == 3 and xs.npieces == 3 and ys.pad == 1 and xs.pad == 1 and xs.C % 64 == 0
+            and ys.C % 64 == 0 and xs.W % 16 == 0 and (ys.B, ys.H, ys.W) == (xs.B, xs.H, xs.W))
 
 
 def conv2d_wgrad3_psa(ys, xs, dw, db, accumulate=True):
