@@ -192,6 +192,13 @@ int64_t ubpl_wgrad3_psa_workspace(int B, int Cin, int Cout, int H, int W);
 int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int Cin,
                     int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,
                     void* stream);
+/* 1x1 weight gradient (+ bias gradient, db nullable) on the 6xbf16 path with
+ * both f32 operands (dy [B,Cout,P], x [B,Cin,P], prologue relu(x*pscale +
+ * pshift) when pscale != nullptr) split while staged.  _workspace: slab floats,
+ * 0 = shape not supported (needs Cin % 128 == 0, Cout % 128 == 0, P % 16 == 0). */
+int64_t ubpl_wgrad1x1_split_load_workspace(int B, int Cin, int Cout, int P);
+int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, int Cin, int Cout, int P, const float* pscale,
+                             const float* pshift, float* slab, float* dw, float* db, int accumulate, void* stream);
 int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                             const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
                             const float* res, float* y, float* slab, int npieces, float* stat_part, void* stream);

@@ -279,3 +279,32 @@ def test_conv1x1_split_load_vs_f64(case):
         e32, esp = _rel(dx32, dxref), _rel(dx, dxref)
         print("sol dgrad %s: f32 %.2e split-load %.2e" % (case, e32, esp))
         assert esp <= 2 * e32 + 1e-8, (esp, e32)
+
+
+@pytest.mark.parametrize("case", [(2, 256, 128, 64, True), (2, 128, 256, 32, True), (3, 256, 256, 16, False),
+                                  (4, 128, 128, 4, True)])
+def test_wgrad1x1_split_load_vs_f64(case):
+    """1x1 weight + bias gradient with both operands split on load, within 2x
+    the exact-f32 kernel's error against float64; accumulate adds."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, Cout, H, pro = case
+    gen = torch.Generator().manual_seed(17 + hash(case) % 1000)
+    x = torch.randn(B, Cin, H, H, generator=gen)
+    dy = torch.randn(B, Cout, H, H, generator=gen)
+    sc, sh = torch.rand(Cin, generator=gen) + 0.5, torch.randn(Cin, generator=gen) * 0.5
+    inp = F.relu((x.double() * sc.double()[None, :, None, None] + sh.double()[None, :, None, None]).float()) \
+        if pro else x
+    dwref = torch.nn.grad.conv2d_weight(inp.double(), (Cout, Cin, 1, 1), dy.double())
+    dbref = dy.double().sum((0, 2, 3))
+    d = lambda t: t.to(DEV)
+    ps, ph = (d(sc), d(sh)) if pro else (None, None)
+    assert Kn.wgrad1x1_split_load_ok(d(dy), d(x))
+    dw = torch.full((Cout, Cin, 1, 1), 0.25, device=DEV)
+    db = torch.full((Cout,), -0.5, device=DEV)
+    Kn.conv2d_wgrad1x1_split_load(d(dy), d(x), dw, db, ps, ph, accumulate=True)
+    dw32, db32 = torch.zeros(Cout, Cin, 1, 1, device=DEV), torch.zeros(Cout, device=DEV)
+    Kn.conv2d_wgrad(d(dy), d(x), 1, 1, dw32, db32, ps, ph, accumulate=False)
+    e32, esp = _rel(dw32, dwref), _rel(dw - 0.25, dwref)
+    print("wgrad1 %s: f32 %.2e split-load %.2e" % (case, e32, esp))
+    assert esp <= 2 * e32 + 1e-8, (esp, e32)
+    assert _rel(db + 0.5, dbref) <= 1e-5

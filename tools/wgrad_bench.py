@@ -34,6 +34,18 @@ def main():
             tp = timeit(lambda: Kn.conv2d_wgrad3_psa(ys, xs, dw, db, accumulate=False), reps)
             line += " | psa %7.3f ms %6.1f TF (splits %d)" % (tp, fl / tp / 1e9, _lib_splits(B, C, H))
         print(line, flush=True)
+    for cin, cout, H in ((256, 128, 64), (128, 256, 64), (256, 256, 64), (256, 128, 32), (128, 256, 32),
+                         (256, 256, 16)):
+        x = torch.randn(B, cin, H, H, device=dev, generator=g)
+        dy = torch.randn(B, cout, H, H, device=dev, generator=g)
+        ps = torch.rand(cin, device=dev, generator=g) + 0.5
+        ph = torch.randn(cin, device=dev, generator=g)
+        dw, db = torch.zeros(cout, cin, 1, 1, device=dev), torch.zeros(cout, device=dev)
+        fl = 2.0 * B * cin * cout * H * H
+        t32 = timeit(lambda: Kn.conv2d_wgrad(dy, x, 1, 1, dw, db, ps, ph, accumulate=False), reps)
+        ts = timeit(lambda: Kn.conv2d_wgrad1x1_split_load(dy, x, dw, db, ps, ph, accumulate=False), reps)
+        print("1x1 wgrad %3d->%3d H=%3d  f32 %7.3f ms %6.1f TF | split-load %7.3f ms %6.1f TF" % (
+            cin, cout, H, t32, fl / t32 / 1e9, ts, fl / ts / 1e9), flush=True)
 
 
 def _lib_splits(B, C, H):

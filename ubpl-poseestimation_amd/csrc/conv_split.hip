@@ -872,6 +872,164 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
     }
 }
 
+// ------------------------------------------------------------------ 1x1 weight gradient, split on load
+// dW[m][k] = sum over pixels n of dy[m][n] * v[k][n], v = relu(x*pscale + pshift)
+// (PRO) or x; db[m] = sum dy[m][n].  GEMM: M = Cout, N = Cin, K = pixels, both
+// operands pixel-contiguous in NCHW (no transposes).  K step = 16 pixels of one
+// image (P % 16 == 0), split over workgroups into a slab [z][Cout][Cin + 1] (last
+// column: the bias gradient, from the Cin-tile-0 workgroups) reduced by
+// conv.hip's wgrad_reduce_kernel.  The f32 operands come global -> registers
+// (two steps ahead), each element is split ONCE per workgroup by the thread
+// that loaded it (thread t: row t/2 of both operands, pixels 8(t&1)..+7), and
+// the pieces go to a double-buffered LDS image [operand][piece][128 rows][32 B]
+// (chunk swizzle c ^ ((row >> 3) & 1), conflict-free ds_read_b128 fragments,
+// conv_psa_kernel's layout).  Tile 128 x 128, wave tile 64 x 64.
+template <bool PRO>
+__global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                          const float* __restrict__ pscale,
+                                                          const float* __restrict__ pshift, int B, int Cin, int Cout,
+                                                          int P, int steps_per_split, float* __restrict__ slab) {
+    constexpr int NP = 3, BM = 128, TM = 2, TN = 2;
+    constexpr int PI = BM * 32;   // one piece image: 128 rows x 16 pixels x 2 B
+    constexpr int OB = NP * PI;   // one operand
+    constexpr int SB = 2 * OB;    // one stage: dy pieces, then x pieces
+    __shared__ __attribute__((aligned(16))) char lds[2 * SB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                              gridDim.x * gridDim.y * gridDim.z);
+    const int bx = lam % gridDim.x, by = (lam / gridDim.x) % gridDim.y, bz = lam / (gridDim.x * gridDim.y);
+    const int m0 = by * BM, c0 = bx * BM;
+    const int psteps = P >> 4;
+    const int total = B * psteps;
+    const int s_begin = bz * steps_per_split;
+    const int s_end = min(total, s_begin + steps_per_split);
+    const int nkt = max(0, s_end - s_begin);
+
+    // loader / splitter: row r of both operands, pixels 8*hp .. 8*hp+7 of the step
+    const int r = tid >> 1, hp = tid & 1;
+    const float* arow = dy + (int64_t)(m0 + r) * P + 8 * hp;
+    const float* brow = x + (int64_t)(c0 + r) * P + 8 * hp;
+    float sc = 1.f, sh = 0.f;
+    if (PRO) {
+        sc = pscale[c0 + r];
+        sh = pshift[c0 + r];
+    }
+    const int wofs = r * 32 + 16 * (hp ^ ((r >> 3) & 1));
+    auto gload = [&](float4 (&a)[2], float4 (&b)[2], int s) {
+        const int bb = s / psteps;
+        const int p0 = (s - bb * psteps) * 16;
+        const float4* a4 = reinterpret_cast<const float4*>(arow + (int64_t)bb * Cout * P + p0);
+        const float4* b4 = reinterpret_cast<const float4*>(brow + (int64_t)bb * Cin * P + p0);
+        a[0] = a4[0];
+        a[1] = a4[1];
+        b[0] = b4[0];
+        b[1] = b4[1];
+    };
+    float bsum = 0.f;
+    auto split_store = [&](int buf, const float4 (&a)[2], const float4 (&b)[2]) {
+        float va[8] = {a[0].x, a[0].y, a[0].z, a[0].w, a[1].x, a[1].y, a[1].z, a[1].w};
+        float vb[8] = {b[0].x, b[0].y, b[0].z, b[0].w, b[1].x, b[1].y, b[1].z, b[1].w};
+        bsum += ((va[0] + va[1]) + (va[2] + va[3])) + ((va[4] + va[5]) + (va[6] + va[7]));
+        if (PRO) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) vb[e] = fmaxf(fmaf(vb[e], sc, sh), 0.f);
+        }
+        uint32_t pa[NP][4], pb[NP][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            uint32_t o[NP], q[NP];
+            split2<NP>(va[2 * e], va[2 * e + 1], o);
+            split2<NP>(vb[2 * e], vb[2 * e + 1], q);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                pa[p][e] = o[p];
+                pb[p][e] = q[p];
+            }
+        }
+        char* base = lds + buf * SB;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            *reinterpret_cast<uint4*>(base + p * PI + wofs) = make_uint4(pa[p][0], pa[p][1], pa[p][2], pa[p][3]);
+            *reinterpret_cast<uint4*>(base + OB + p * PI + wofs) = make_uint4(pb[p][0], pb[p][1], pb[p][2], pb[p][3]);
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+    const int li = lane & 31, h = lane >> 5;
+
+    float4 cA[2], cB[2], nA[2], nB[2];
+    if (nkt > 0) gload(cA, cB, s_begin);
+    if (nkt > 1) gload(nA, nB, s_begin + 1);
+    for (int t = 0; t < nkt; ++t) {
+        // buffer t&1 was last read in step t-2, before every wave's step t-1 barrier
+        split_store(t & 1, cA, cB);
+        cA[0] = nA[0];
+        cA[1] = nA[1];
+        cB[0] = nB[0];
+        cB[1] = nB[1];
+        if (t + 2 < nkt) gload(nA, nB, s_begin + t + 2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const char* base = lds + (t & 1) * SB;
+        bf16x8 af[TM][NP], bfr[TN][NP];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int row = wm + 32 * i + li;
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                af[i][p] = *reinterpret_cast<const bf16x8*>(base + p * PI + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int row = wn + 32 * j + li;
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                bfr[j][p] =
+                    *reinterpret_cast<const bf16x8*>(base + OB + p * PI + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+        }
+        floatx16 tmp[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) tmp[i][j][q] = 0.f;
+                mfma_split<NP>(tmp[i][j], af[i], bfr[j]);
+            }
+        __builtin_amdgcn_sched_barrier(0);   // chains first, adds after (see conv_psa_kernel)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] += tmp[i][j];
+    }
+
+    const int Nt = Cin + 1;
+    float* sl = slab + (int64_t)bz * Cout * Nt;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = c0 + wn + 32 * j + li;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int m = m0 + wm + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+                sl[(int64_t)m * Nt + n] = acc[i][j][q];
+            }
+    }
+    // bias gradient: the two threads of a row hold its two pixel halves
+    const float bt = bsum + __shfl_xor(bsum, 1, 64);
+    if (bx == 0 && hp == 0) sl[(int64_t)(m0 + r) * Nt + Cin] = bt;
+}
+
 // y[b,m,p] = sum_z slab[z][m][b*P+p] + bias[m] (+ res)
 __global__ void __launch_bounds__(256) split_reduce_kernel(const float* __restrict__ slab, int splits, int Cout, int P,
                                                           int64_t N, const float* __restrict__ bias, const float* res,
@@ -1318,4 +1476,54 @@ UBPL_API int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t
                            H, W, per, slab);
     UBPL_LAUNCH_CHECK();
     return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 9, db != nullptr, dw, db, accumulate, stream);
+}
+
+// ---- 1x1 weight gradient with the split on load
+namespace {
+bool wgrad1_sol_supported(int B, int Cin, int Cout, int P) {
+    return B > 0 && Cin % 128 == 0 && Cout % 128 == 0 && P % 16 == 0 && P > 0 &&
+           (int64_t)B * Cin * P < (1LL << 31) && (int64_t)B * Cout * P < (1LL << 31);
+}
+
+int wgrad1_sol_splits(int B, int Cin, int Cout, int P) {
+    const int tiles = (Cin / 128) * (Cout / 128);
+    const int steps = B * (P / 16);
+    int s = 512 / tiles;                                    // one round of 2 workgroups per CU
+    if (s < 1) s = 1;
+    if (s > steps / 8) s = steps / 8 > 0 ? steps / 8 : 1;   // >= 8 K steps per split
+    const int per = (steps + s - 1) / s;
+    return (steps + per - 1) / per;
+}
+}  // namespace
+
+// Floats of slab ubpl_wgrad1x1_split_load needs; 0 = shape not supported
+// (Cin % 128, Cout % 128, P % 16): use ubpl_conv2d_wgrad.
+UBPL_API int64_t ubpl_wgrad1x1_split_load_workspace(int B, int Cin, int Cout, int P) {
+    if (!wgrad1_sol_supported(B, Cin, Cout, P)) return 0;
+    return (int64_t)wgrad1_sol_splits(B, Cin, Cout, P) * Cout * (Cin + 1);
+}
+
+// dw[Cout,Cin,1,1] (+)= 1x1 weight gradient, db[Cout] (+)= sum dy (nullable),
+// on the 6xbf16 path with both f32 operands split while they are staged
+// (wgrad1_sol_kernel): dy [B,Cout,P], x [B,Cin,P], v = relu(x*pscale + pshift)
+// when pscale != nullptr.  16-B aligned dy / x.
+UBPL_API int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, int Cin, int Cout, int P,
+                                      const float* pscale, const float* pshift, float* slab, float* dw, float* db,
+                                      int accumulate, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (!wgrad1_sol_supported(B, Cin, Cout, P) || slab == nullptr || (((uintptr_t)dy) & 15) ||
+        (((uintptr_t)x) & 15))
+        return (int)hipErrorInvalidValue;
+    const int splits = wgrad1_sol_splits(B, Cin, Cout, P);
+    const int steps = B * (P / 16);
+    const int per = (steps + splits - 1) / splits;
+    dim3 grid((unsigned)(Cin / 128), (unsigned)(Cout / 128), (unsigned)splits);
+    if (pscale != nullptr)
+        hipLaunchKernelGGL((wgrad1_sol_kernel<true>), grid, dim3(NT), 0, st, dy, x, pscale, pshift, B, Cin, Cout, P,
+                           per, slab);
+    else
+        hipLaunchKernelGGL((wgrad1_sol_kernel<false>), grid, dim3(NT), 0, st, dy, x, pscale, pshift, B, Cin, Cout, P,
+                           per, slab);
+    UBPL_LAUNCH_CHECK();
+    return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 1, db != nullptr, dw, db, accumulate, stream);
 }

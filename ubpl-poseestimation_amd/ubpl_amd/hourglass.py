@@ -34,6 +34,8 @@ BN_MOMENTUM = 0.1
 _PRODUCER_STATS = os.environ.get("UBPL_PRODUCER_STATS", "1") != "0"
 # 64-channel 3x3 weight gradients on the split path (UBPL_WGRAD3_64=0: exact-f32 kernel)
 _WGRAD3_64 = os.environ.get("UBPL_WGRAD3_64", "1") != "0"
+# 1x1 weight gradients on the 6xbf16 split-on-load kernel (UBPL_WGRAD1_SPLIT=0: exact-f32 kernel)
+_WGRAD1_SPLIT = os.environ.get("UBPL_WGRAD1_SPLIT", "1") != "0"
 
 
 # ---------------------------------------------------------------------------
@@ -588,6 +590,10 @@ class _Exec:
 
     def wgrad(self, name, dy, x, KS, stride=1, pro=None):
         ps, ph = (None, None) if pro is None else pro
+        if KS == 1 and self.m.conv_pieces == 3 and _WGRAD1_SPLIT and Kn.wgrad1x1_split_load_ok(dy, x):
+            Kn.conv2d_wgrad1x1_split_load(dy, x, self.m.G(name + ".weight"), self.m.G(name + ".bias"), ps, ph,
+                                          accumulate=True)
+            return
         Kn.conv2d_wgrad(dy, x, KS, stride, self.m.G(name + ".weight"), self.m.G(name + ".bias"), ps, ph,
                         accumulate=True)
 

@@ -327,6 +327,23 @@ def conv2d_wgrad(dy, x, KS, stride, dw, db, pscale=None, pshift=None, accumulate
          _p(slab), _p(dw), _p(db), int(accumulate), stream())
 
 
+def wgrad1x1_split_load_ok(dy, x):
+    B, Cin, H, W = x.shape
+    return (dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0
+            and _lib.lib().ubpl_wgrad1x1_split_load_workspace(B, Cin, dy.shape[1], H * W) > 0)
+
+
+def conv2d_wgrad1x1_split_load(dy, x, dw, db, pscale=None, pshift=None, accumulate=True):
+    """1x1 weight (+ bias) gradient on the 6xbf16 path, f32 operands split on load
+    (v = relu(x*pscale + pshift) when pscale is given)."""
+    B, Cin, H, W = x.shape
+    Cout = dy.shape[1]
+    n = _lib.lib().ubpl_wgrad1x1_split_load_workspace(B, Cin, Cout, H * W)
+    slab = torch.empty(int(n), device=x.device, dtype=F32)
+    call("ubpl_wgrad1x1_split_load", _p(dy), _p(x), B, Cin, Cout, H * W, _p(pscale), _p(pshift), _p(slab), _p(dw),
+         _p(db), int(accumulate), stream())
+
+
 def conv_weight_flip(w):
     """Data-gradient weights (stride 1), viewed as [Cin, KS*KS, Cout]."""
     Cout, Cin, KS, _ = w.shape
