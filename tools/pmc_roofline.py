@@ -20,7 +20,7 @@ import re
 import sys
 
 PATS = {"f32": re.compile(r"conv_fwd_kernel<(\d+), 128, 3, 1, true, false"),
-        "psa": re.compile(r"conv_psa_kernel<(\d+), 3, 3>")}
+        "psa": re.compile(r"conv_psa_kernel<(\d+), 3, 3(, \d+, \d+)?>")}
 PAT = PATS["f32"]
 
 
