@@ -110,18 +110,25 @@ int ubpl_bn_partials(const float* y, int B, int C, int P, float* part, void* str
 int ubpl_bn_stats_from_partials(const float* part, int C, int64_t N, const float* gamma,
                                 const float* beta, float eps, float momentum, float* rmean, float* rvar,
                                 float* mean_out, float* invstd_out, float* scale, float* shift_out, void* stream);
+/* Backward of y = [relu](bn(x)); dgamma/dbeta accumulate; dx = add1 + add2 + dL/dx.
+ * part: ubpl_bn_partial_floats(C, B*HW) floats = per (channel, 64-pixel slice)
+ * (S1, S2) = (sum g, sum g*(x - mean)), g = dz under the recomputed ReLU mask;
+ * part_ready = 1: dz's producer already wrote them (a conv epilogue's bn_part
+ * argument) and no statistics pass runs; coef: 3*C floats of scratch. */
+int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma, const float* mean,
+                     const float* invstd, const float* scale, const float* shift, int relu, float* part,
+                     int part_ready, float* coef, float* dgamma, float* dbeta, const float* add1, const float* add2,
+                     float* dx, void* stream);
 /* The same backward with dx delivered only as PSA planes (ubpl_split_activation
  * layout, border `pad`, npieces 2 or 3) — the operand of a split-path 3x3 data /
  * weight gradient; no addends; C % 16 == 0. */
 int ubpl_bn_backward_split(const float* dz, const float* x, int B, int C, int H, int W, const float* gamma,
                            const float* mean, const float* invstd, const float* scale, const float* shift, int relu,
-                           double* part, float* coef, float* dgamma, float* dbeta, int pad, int npieces,
-                           uint16_t* dst, int64_t plane, void* stream);
-/* Backward of y = [relu](bn(x)); dgamma/dbeta accumulate; dx = add1 + add2 + dL/dx. */
-int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma, const float* mean,
-                     const float* invstd, const float* scale, const float* shift, int relu, double* part,
-                     float* coef, float* dgamma, float* dbeta, const float* add1, const float* add2, float* dx,
-                     void* stream);
+                           float* part, int part_ready, float* coef, float* dgamma, float* dbeta, int pad,
+                           int npieces, uint16_t* dst, int64_t plane, void* stream);
+/* The backward statistics partials alone (the layout above). */
+int ubpl_bn_backward_partials(const float* dz, const float* x, int B, int C, int HW, const float* scale,
+                              const float* shift, const float* mean, int relu, float* part, void* stream);
 
 /* Conv (models/base/layers.py:31-50): 1x1/s1, 3x3/s1, 7x7/s2, pad (KS-1)/2,
  * optional fused pre-activation relu(x*pscale + pshift), bias, residual add

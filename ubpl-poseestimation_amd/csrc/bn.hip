@@ -28,7 +28,8 @@ namespace {
 // write-through: no release fence, which would write back the whole L2),
 // drains them, and takes a ticket; the block drawing the last ticket reads the
 // channel's partials with agent-scope atomic loads (sc1: past any stale L1
-// line) in slice order (deterministic) and resets the counter.
+// line), one slice per lane, sums them in a fixed order (deterministic) and
+// resets the counter.
 __device__ __forceinline__ void publish2(double* p, double a, double b) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(a),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -47,6 +48,32 @@ __device__ __forceinline__ bool last_arriver(unsigned* cnt, unsigned n) {
     if (old != n - 1) return false;
     __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
+}
+
+// Wave 0 of every (channel, slice) block publishes the slice's two sums and
+// takes a ticket; in the channel's last block the 64 lanes read the slices in
+// parallel (one round trip, not one per slice: a serial read chain here was
+// ~10 % of the training step) and sum them in a fixed tree order
+// (deterministic).  Returns true in lane 0 of that block, with the totals.
+__device__ __forceinline__ bool combine_slices(double* pc, int sp, int nsp, unsigned* cnt, double d1, double d2,
+                                               double& t1, double& t2) {
+    if (threadIdx.x >= 64) return false;
+    const int lane = threadIdx.x;
+    int last = 0;
+    if (lane == 0) {
+        publish2(pc + sp * 2, d1, d2);
+        last = last_arriver(cnt, nsp) ? 1 : 0;
+    }
+    if (!__shfl(last, 0, 64)) return false;
+    t1 = 0.0;
+    t2 = 0.0;
+    for (int q = lane; q < nsp; q += 64) {
+        t1 += consume(pc + q * 2);
+        t2 += consume(pc + q * 2 + 1);
+    }
+    t1 = ubpl::wave_sum(t1);
+    t2 = ubpl::wave_sum(t2);
+    return lane == 0;
 }
 
 struct StatsOut {
@@ -90,15 +117,8 @@ __global__ void __launch_bounds__(256) stats_kernel(const float* __restrict__ x,
     }
     const double d1 = ubpl::block_sum((double)s1, red);
     const double d2 = ubpl::block_sum((double)s2, red);
-    if (threadIdx.x != 0) return;
-    double* pc = part + (int64_t)c * gridDim.y * 2;
-    publish2(pc + sp * 2, d1, d2);
-    if (!last_arriver(cnt + c, gridDim.y)) return;
-    double t1 = 0.0, t2 = 0.0;
-    for (int q = 0; q < (int)gridDim.y; ++q) {
-        t1 += consume(pc + q * 2);
-        t2 += consume(pc + q * 2 + 1);
-    }
+    double t1, t2;
+    if (!combine_slices(part + (int64_t)c * gridDim.y * 2, sp, gridDim.y, cnt + c, d1, d2, t1, t2)) return;
     const int64_t N = (int64_t)B * HW;
     const double m1 = t1 / (double)N;
     double var = t2 / (double)N - m1 * m1;
@@ -151,77 +171,114 @@ __global__ void __launch_bounds__(256) apply_kernel(const float* __restrict__ x,
     }
 }
 
+// Finalize kernels: one 1024-thread block per channel, NPT independent slice
+// loads per thread before any add (a dependent load-add chain made each
+// finalize launch latency-bound, ~15 us on the training step's critical path).
+constexpr int FT = 1024, NPT = 8;
+
 struct BwdOut {
     const float* gamma;
     const float* invstd;
     float *dgamma, *dbeta, *ca, *cb, *cc;
 };
 
-// Per (channel, slice): S1 = sum dyp, S2 = sum dyp*(x - mean) with the ReLU
-// mask recomputed; the channel's last block produces dgamma/dbeta and the
-// coefficients of dx = a*dyp + b*(x - mean) + c.
+// Backward statistics, per (channel c, 64-pixel slice q of the flat (b, p)
+// range): part[(c*np + q)*2 + {0,1}] = (S1, S2) = (sum g, sum g*(x - mean)),
+// g = dz with the ReLU mask recomputed.  Plain stores, no atomics: the
+// channel's totals come from bn_bwd_finalize_kernel (a last-arriver hand-off
+// through memory-side atomics cost ~10 % of the training step).  One wave per
+// 4 slices of one channel: lane l takes pixels 4l..4l+3 (float4; P % 4 == 0),
+// a 16-lane row is one slice (DPP row sums).  The conv epilogues write the same
+// layout (common.h tile_bn_bwd_partials).
 template <bool VEC>
-__global__ void __launch_bounds__(256) bwd_stats_kernel(const float* __restrict__ dz, const float* __restrict__ x,
-                                                       int B, int C, int HW, int bper,
-                                                       const float* __restrict__ scale,
-                                                       const float* __restrict__ shift,
-                                                       const float* __restrict__ mean, int relu,
-                                                       double* __restrict__ part, unsigned* __restrict__ cnt,
-                                                       BwdOut o) {
-    __shared__ double red[16];
-    const int c = blockIdx.x, sp = blockIdx.y;
-    const int b0 = sp * bper, b1 = min(B, b0 + bper);
+__global__ void __launch_bounds__(256) bn_bwd_partials_kernel(const float* __restrict__ dz,
+                                                             const float* __restrict__ x, int C, int P, int64_t N,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean, int relu,
+                                                             float* __restrict__ part) {
+    constexpr int IT = 4;   // 256-pixel chunks (4 slices each) per wave
+    const int64_t np = (N + 63) / 64, nw = (np + 4 * IT - 1) / (4 * IT);
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= (int64_t)C * nw) return;
+    const int lane = threadIdx.x & 63;
+    const int c = (int)(w / nw);
+    const int64_t u0 = (w - (int64_t)c * nw) * IT;
     const float sc = scale[c], sh = shift[c], mu = mean[c];
-    float s1 = 0.f, s2 = 0.f;
-    if (VEC) {
-        const int hw4 = HW >> 2;
-        const int n4 = (b1 - b0) * hw4;
-        const float4* x4 = reinterpret_cast<const float4*>(x);
-        const float4* d4 = reinterpret_cast<const float4*>(dz);
-        for (int i = threadIdx.x; i < n4; i += blockDim.x) {
-            const int bb = i / hw4, o4 = i - bb * hw4;
-            const int64_t off = ((int64_t)(b0 + bb) * C + c) * hw4 + o4;
-            const float4 xv = x4[off];
-            float4 g = d4[off];
-            if (relu) {
-                g.x = fmaf(xv.x, sc, sh) > 0.f ? g.x : 0.f;
-                g.y = fmaf(xv.y, sc, sh) > 0.f ? g.y : 0.f;
-                g.z = fmaf(xv.z, sc, sh) > 0.f ? g.z : 0.f;
-                g.w = fmaf(xv.w, sc, sh) > 0.f ? g.w : 0.f;
+    float g[IT][4], xv[IT][4];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {   // all loads first
+        const int64_t n0 = (u0 + it) * 256 + 4 * lane;
+        if (VEC) {   // P % 4 == 0, 16-B aligned: the lane's 4 pixels are one float4 of one image
+            const int64_t nc = n0 < N ? n0 : 0;
+            const int64_t b = nc / P;
+            const int64_t off = (b * C + c) * P + (nc - b * P);
+            const float4 gv = *reinterpret_cast<const float4*>(dz + off);
+            const float4 xq = *reinterpret_cast<const float4*>(x + off);
+            g[it][0] = gv.x, g[it][1] = gv.y, g[it][2] = gv.z, g[it][3] = gv.w;
+            xv[it][0] = xq.x, xv[it][1] = xq.y, xv[it][2] = xq.z, xv[it][3] = xq.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t nc = n0 + e < N ? n0 + e : 0;
+                const int64_t b = nc / P;
+                const int64_t off = (b * C + c) * P + (nc - b * P);
+                g[it][e] = dz[off];
+                xv[it][e] = x[off];
             }
-            s1 += (g.x + g.y) + (g.z + g.w);
-            s2 = fmaf(g.x, xv.x - mu, fmaf(g.y, xv.y - mu, fmaf(g.z, xv.z - mu, fmaf(g.w, xv.w - mu, s2))));
-        }
-    } else {
-        const int n = (b1 - b0) * HW;
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const int bb = i / HW, o1 = i - bb * HW;
-            const int64_t off = ((int64_t)(b0 + bb) * C + c) * HW + o1;
-            const float xv = x[off];
-            float g = dz[off];
-            if (relu && !(fmaf(xv, sc, sh) > 0.f)) g = 0.f;
-            s1 += g;
-            s2 = fmaf(g, xv - mu, s2);
         }
     }
-    const double d1 = ubpl::block_sum((double)s1, red);
-    const double d2 = ubpl::block_sum((double)s2, red);
-    if (threadIdx.x != 0) return;
-    double* pc = part + (int64_t)c * gridDim.y * 2;
-    publish2(pc + sp * 2, d1, d2);
-    if (!last_arriver(cnt + c, gridDim.y)) return;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int64_t n0 = (u0 + it) * 256 + 4 * lane;
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float ge = n0 + e < N ? g[it][e] : 0.f;
+            if (relu && !(fmaf(xv[it][e], sc, sh) > 0.f)) ge = 0.f;
+            s1 += ge;
+            s2 = fmaf(ge, xv[it][e] - mu, s2);
+        }
+        s1 = ubpl::row_sum16(s1);
+        s2 = ubpl::row_sum16(s2);
+        const int64_t q = (u0 + it) * 4 + (lane >> 4);
+        if ((lane & 15) == 15 && q < np) {
+            part[((int64_t)c * np + q) * 2] = s1;
+            part[((int64_t)c * np + q) * 2 + 1] = s2;
+        }
+    }
+}
+
+// Channel totals of the backward partials in f64 (fixed order): dgamma +=
+// S2*invstd, dbeta += S1, and the coefficients of dx = a*g + b*(x - mean) + c.
+__global__ void __launch_bounds__(FT) bn_bwd_finalize_kernel(const float* __restrict__ part, int64_t np, int64_t N,
+                                                            BwdOut o) {
+    __shared__ double red[16];
+    const int c = blockIdx.x;
+    const float2* pc = reinterpret_cast<const float2*>(part) + (int64_t)c * np;
     double t1 = 0.0, t2 = 0.0;
-    for (int q = 0; q < (int)gridDim.y; ++q) {
-        t1 += consume(pc + q * 2);
-        t2 += consume(pc + q * 2 + 1);
+    for (int64_t q0 = 0; q0 < np; q0 += (int64_t)FT * NPT) {
+        float2 v[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {   // independent loads first
+            const int64_t q = q0 + threadIdx.x + (int64_t)k * FT;
+            v[k] = q < np ? pc[q] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            t1 += (double)v[k].x;
+            t2 += (double)v[k].y;
+        }
     }
-    const double N = (double)((int64_t)B * HW);
+    t1 = ubpl::block_sum(t1, red);
+    t2 = ubpl::block_sum(t2, red);
+    if (threadIdx.x != 0) return;
     const double is = o.invstd[c], g = o.gamma[c];
     if (o.dgamma) o.dgamma[c] += (float)(t2 * is);
     if (o.dbeta) o.dbeta[c] += (float)t1;
     o.ca[c] = (float)(g * is);
-    o.cb[c] = (float)(-g * is * is * is * t2 / N);
-    o.cc[c] = (float)(-g * is * t1 / N);
+    o.cb[c] = (float)(-g * is * is * is * t2 / (double)N);
+    o.cc[c] = (float)(-g * is * t1 / (double)N);
 }
 
 __device__ __forceinline__ float bwd_one(float g, float xv, float sc, float sh, float mu, float a, float b, float c,
@@ -330,20 +387,59 @@ __global__ void __launch_bounds__(256) bn_partials_kernel(const float* __restric
 }
 
 // mean = sum S / N; M2 = sum M2_q + sum n_q (S_q/n_q - mean)^2, in f64.
-__global__ void __launch_bounds__(256) bn_finalize_partials_kernel(const float* __restrict__ part, int64_t np,
-                                                                  int64_t N, StatsOut o) {
+__global__ void __launch_bounds__(FT) bn_finalize_partials_kernel(const float* __restrict__ part, int64_t np,
+                                                                 int64_t N, StatsOut o) {
     __shared__ double red[16];
     const int c = blockIdx.x;
-    const float* pc = part + (int64_t)c * np * 2;
+    const float2* pc = reinterpret_cast<const float2*>(part) + (int64_t)c * np;
+    auto nq_of = [&](int64_t q) { return (double)(N - q * 64 < 64 ? N - q * 64 : 64); };
     double t1 = 0.0;
-    for (int64_t q = threadIdx.x; q < np; q += blockDim.x) t1 += (double)pc[q * 2];
+    float2 v[NPT];   // the first FT*NPT slices stay in registers for the second pass
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const int64_t q = threadIdx.x + (int64_t)k * FT;
+        v[k] = q < np ? pc[q] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) t1 += (double)v[k].x;
+    for (int64_t q0 = (int64_t)FT * NPT; q0 < np; q0 += (int64_t)FT * NPT) {
+        float w[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const int64_t q = q0 + threadIdx.x + (int64_t)k * FT;
+            w[k] = q < np ? pc[q].x : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) t1 += (double)w[k];
+    }
     t1 = ubpl::block_sum(t1, red);
     const double mean = t1 / (double)N;
     double t2 = 0.0;
-    for (int64_t q = threadIdx.x; q < np; q += blockDim.x) {
-        const double nq = (double)(N - q * 64 < 64 ? N - q * 64 : 64);
-        const double dm = (double)pc[q * 2] / nq - mean;
-        t2 += (double)pc[q * 2 + 1] + nq * dm * dm;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const int64_t q = threadIdx.x + (int64_t)k * FT;
+        if (q < np) {
+            const double nq = nq_of(q);
+            const double dm = (double)v[k].x / nq - mean;
+            t2 += (double)v[k].y + nq * dm * dm;
+        }
+    }
+    for (int64_t q0 = (int64_t)FT * NPT; q0 < np; q0 += (int64_t)FT * NPT) {
+        float2 w[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const int64_t q = q0 + threadIdx.x + (int64_t)k * FT;
+            w[k] = q < np ? pc[q] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            const int64_t q = q0 + threadIdx.x + (int64_t)k * FT;
+            if (q < np) {
+                const double nq = nq_of(q);
+                const double dm = (double)w[k].x / nq - mean;
+                t2 += (double)w[k].y + nq * dm * dm;
+            }
+        }
     }
     t2 = ubpl::block_sum(t2, red);
     if (threadIdx.x != 0) return;
@@ -383,7 +479,7 @@ UBPL_API int ubpl_bn_stats_from_partials(const float* part, int C, int64_t N, co
                                          float* mean_out, float* invstd_out, float* scale, float* shift_out,
                                          void* stream) {
     StatsOut o{gamma, beta, eps, momentum, rmean, rvar, mean_out, invstd_out, scale, shift_out};
-    hipLaunchKernelGGL(bn_finalize_partials_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part,
+    hipLaunchKernelGGL(bn_finalize_partials_kernel, dim3(C), dim3(FT), 0, (hipStream_t)stream, part,
                        (N + 63) / 64, N, o);
     UBPL_LAUNCH_CHECK();
     return 0;
@@ -467,73 +563,98 @@ __global__ void __launch_bounds__(256) bwd_apply_split_kernel(const float* __res
     ubpl::store_psa_row<NP>(v, dst + (((int64_t)(b * G + g) * Hp + hp) * Wp + wq) * 16, plane);
 }
 
-// ubpl_bn_backward with dx delivered as PSA planes only (no f32 dx, no
-// addends): statistics pass, then bwd_apply_split_kernel.  C % 16 == 0.
-UBPL_API int ubpl_bn_backward_split(const float* dz, const float* x, int B, int C, int H, int W, const float* gamma,
-                                    const float* mean, const float* invstd, const float* scale, const float* shift,
-                                    int relu, double* part, float* coef, float* dgamma, float* dbeta, int pad,
-                                    int npieces, uint16_t* dst, int64_t plane, void* stream) {
-    const int HW = H * W;
-    if (C % 16 != 0 || C > MAXBN || npieces < 2 || npieces > 3 || pad < 0) return (int)hipErrorInvalidValue;
-    const int splits = splits_for(B, C);
-    const int bper = (B + splits - 1) / splits;
-    const int gs = (B + bper - 1) / bper;
-    const bool vec = (HW % 4 == 0) && ((((uintptr_t)dz | (uintptr_t)x) & 15) == 0);
-    float* ca = coef;
-    float* cb = coef + C;
-    float* cc = coef + 2 * C;
-    unsigned* cnt = reinterpret_cast<unsigned*>(part);
-    part += CNT_DOUBLES;
-    const BwdOut o{gamma, invstd, dgamma, dbeta, ca, cb, cc};
-    if (vec)
-        hipLaunchKernelGGL(bwd_stats_kernel<true>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
-                           bper, scale, shift, mean, relu, part, cnt, o);
-    else
-        hipLaunchKernelGGL(bwd_stats_kernel<false>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
-                           bper, scale, shift, mean, relu, part, cnt, o);
+namespace {
+// statistics -> coefficients: the partials pass (unless the producer's
+// epilogue wrote them: part_ready), then the f64 finalize
+int bwd_stats(const float* dz, const float* x, int B, int C, int HW, const float* gamma, const float* mean,
+              const float* invstd, const float* scale, const float* shift, int relu, float* part, int part_ready,
+              float* coef, float* dgamma, float* dbeta, hipStream_t st) {
+    const int64_t N = (int64_t)B * HW;
+    const int64_t np = (N + 63) / 64;
+    if (!part_ready) {
+        const bool vec = (HW % 4 == 0) && ((((uintptr_t)dz | (uintptr_t)x) & 15) == 0);
+        const int64_t waves = (int64_t)C * ((np + 15) / 16);
+        const dim3 grid((unsigned)((waves + 3) / 4));
+        if (vec)
+            hipLaunchKernelGGL(bn_bwd_partials_kernel<true>, grid, dim3(256), 0, st, dz, x, C, HW, N, scale, shift,
+                               mean, relu, part);
+        else
+            hipLaunchKernelGGL(bn_bwd_partials_kernel<false>, grid, dim3(256), 0, st, dz, x, C, HW, N, scale, shift,
+                               mean, relu, part);
+        UBPL_LAUNCH_CHECK();
+    }
+    const BwdOut o{gamma, invstd, dgamma, dbeta, coef, coef + C, coef + 2 * C};
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(FT), 0, st, part, np, N, o);
     UBPL_LAUNCH_CHECK();
-    const int Hp = H + 2 * pad, Wp = W + 2 * pad;
-    dim3 grid((unsigned)((Hp * Wp + 255) / 256), (unsigned)(C / 16), (unsigned)B);
-    if (npieces == 3)
-        hipLaunchKernelGGL(bwd_apply_split_kernel<3>, grid, dim3(256), 0, (hipStream_t)stream, dz, x, C, H, W, scale,
-                           shift, mean, relu, ca, cb, cc, pad, dst, plane);
+    return 0;
+}
+}  // namespace
+
+// Backward statistics partials of dz (ReLU mask from x's BN) alone: the layout
+// ubpl_bn_backward(..., part_ready = 1) takes; part: ubpl_bn_partial_floats(C, B*HW).
+UBPL_API int ubpl_bn_backward_partials(const float* dz, const float* x, int B, int C, int HW, const float* scale,
+                                       const float* shift, const float* mean, int relu, float* part, void* stream) {
+    const int64_t N = (int64_t)B * HW;
+    const int64_t np = (N + 63) / 64;
+    const bool vec = (HW % 4 == 0) && ((((uintptr_t)dz | (uintptr_t)x) & 15) == 0);
+    const int64_t waves = (int64_t)C * ((np + 15) / 16);
+    const dim3 grid((unsigned)((waves + 3) / 4));
+    if (vec)
+        hipLaunchKernelGGL(bn_bwd_partials_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, dz, x, C, HW, N,
+                           scale, shift, mean, relu, part);
     else
-        hipLaunchKernelGGL(bwd_apply_split_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream, dz, x, C, H, W, scale,
-                           shift, mean, relu, ca, cb, cc, pad, dst, plane);
+        hipLaunchKernelGGL(bn_bwd_partials_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, dz, x, C, HW, N,
+                           scale, shift, mean, relu, part);
     UBPL_LAUNCH_CHECK();
     return 0;
 }
 
+// ubpl_bn_backward with dx delivered as PSA planes only (no f32 dx, no
+// addends): statistics, then bwd_apply_split_kernel.  C % 16 == 0.
+UBPL_API int ubpl_bn_backward_split(const float* dz, const float* x, int B, int C, int H, int W, const float* gamma,
+                                    const float* mean, const float* invstd, const float* scale, const float* shift,
+                                    int relu, float* part, int part_ready, float* coef, float* dgamma, float* dbeta,
+                                    int pad, int npieces, uint16_t* dst, int64_t plane, void* stream) {
+    const int HW = H * W;
+    if (C % 16 != 0 || npieces < 2 || npieces > 3 || pad < 0) return (int)hipErrorInvalidValue;
+    hipStream_t st = (hipStream_t)stream;
+    const int e = bwd_stats(dz, x, B, C, HW, gamma, mean, invstd, scale, shift, relu, part, part_ready, coef, dgamma,
+                            dbeta, st);
+    if (e) return e;
+    const float *ca = coef, *cb = coef + C, *cc = coef + 2 * C;
+    const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+    dim3 grid((unsigned)((Hp * Wp + 255) / 256), (unsigned)(C / 16), (unsigned)B);
+    if (npieces == 3)
+        hipLaunchKernelGGL(bwd_apply_split_kernel<3>, grid, dim3(256), 0, st, dz, x, C, H, W, scale, shift, mean,
+                           relu, ca, cb, cc, pad, dst, plane);
+    else
+        hipLaunchKernelGGL(bwd_apply_split_kernel<2>, grid, dim3(256), 0, st, dz, x, C, H, W, scale, shift, mean,
+                           relu, ca, cb, cc, pad, dst, plane);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// dx = BatchNorm(+ReLU) backward of dz (+ add1 + add2), dgamma/dbeta (+)= ;
+// part: ubpl_bn_partial_floats(C, B*HW) floats of scratch, or the backward
+// partials the producer of dz already wrote (part_ready = 1); coef: 3*C floats.
 UBPL_API int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma,
                               const float* mean, const float* invstd, const float* scale, const float* shift,
-                              int relu, double* part, float* coef, float* dgamma, float* dbeta, const float* add1,
-                              const float* add2, float* dx, void* stream) {
-    const int splits = splits_for(B, C);
-    const int bper = (B + splits - 1) / splits;
-    const int gs = (B + bper - 1) / bper;
+                              int relu, float* part, int part_ready, float* coef, float* dgamma, float* dbeta,
+                              const float* add1, const float* add2, float* dx, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const int e = bwd_stats(dz, x, B, C, HW, gamma, mean, invstd, scale, shift, relu, part, part_ready, coef, dgamma,
+                            dbeta, st);
+    if (e) return e;
     const uintptr_t al = (uintptr_t)dz | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)add1 | (uintptr_t)add2;
     const bool vec = (HW % 4 == 0) && ((al & 15) == 0);
-    float* ca = coef;
-    float* cb = coef + C;
-    float* cc = coef + 2 * C;
-    if (C > MAXBN) return (int)hipErrorInvalidValue;
-    unsigned* cnt = reinterpret_cast<unsigned*>(part);
-    part += CNT_DOUBLES;
-    const BwdOut o{gamma, invstd, dgamma, dbeta, ca, cb, cc};
-    if (vec)
-        hipLaunchKernelGGL(bwd_stats_kernel<true>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
-                           bper, scale, shift, mean, relu, part, cnt, o);
-    else
-        hipLaunchKernelGGL(bwd_stats_kernel<false>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, dz, x, B, C, HW,
-                           bper, scale, shift, mean, relu, part, cnt, o);
-    UBPL_LAUNCH_CHECK();
+    const float *ca = coef, *cb = coef + C, *cc = coef + 2 * C;
     const int64_t total = (int64_t)B * C * HW;
     if (vec)
-        hipLaunchKernelGGL(bwd_apply_vec_kernel, dim3(grid_ew(total / 4)), dim3(256), 0, (hipStream_t)stream, dz, x, C,
-                           HW / 4, total / 4, scale, shift, mean, relu, ca, cb, cc, add1, add2, dx);
+        hipLaunchKernelGGL(bwd_apply_vec_kernel, dim3(grid_ew(total / 4)), dim3(256), 0, st, dz, x, C, HW / 4,
+                           total / 4, scale, shift, mean, relu, ca, cb, cc, add1, add2, dx);
     else
-        hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_ew(total)), dim3(256), 0, (hipStream_t)stream, dz, x, C, HW,
-                           total, scale, shift, mean, relu, ca, cb, cc, add1, add2, dx);
+        hipLaunchKernelGGL(bwd_apply_kernel, dim3(grid_ew(total)), dim3(256), 0, st, dz, x, C, HW, total, scale,
+                           shift, mean, relu, ca, cb, cc, add1, add2, dx);
     UBPL_LAUNCH_CHECK();
     return 0;
 }

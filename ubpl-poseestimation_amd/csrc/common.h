@@ -166,6 +166,13 @@ __device__ __forceinline__ float dpp_add(float v) {
     return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
                                                                      true));
 }
+// Sum over each 16-lane row (lane 15 of the row holds it).
+__device__ __forceinline__ float row_sum16(float v) {
+    v = dpp_add<0x111>(v);   // row_shr:1
+    v = dpp_add<0x112>(v);   // row_shr:2
+    v = dpp_add<0x114>(v);   // row_shr:4
+    return dpp_add<0x118>(v);   // row_shr:8
+}
 __device__ __forceinline__ float half_sum_dpp(float v) {
     v = dpp_add<0x111>(v);   // row_shr:1
     v = dpp_add<0x112>(v);   // row_shr:2

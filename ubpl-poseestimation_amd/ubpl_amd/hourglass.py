@@ -578,14 +578,15 @@ class _Exec:
     def _coef(self):
         return self.m._ws[("coef", self.B)]
 
-    def bn_bwd(self, name, dz, x, relu, add1=None, add2=None, out=None):
+    def bn_bwd(self, name, dz, x, relu, add1=None, add2=None, out=None, part=None):
+        """part: the backward partials dz's producer wrote (None: a statistics pass)."""
         sc, sh, mu, istd = self.bnc(name)
-        return Kn.bn_backward(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.part, self._coef(),
+        return Kn.bn_backward(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, part, self._coef(),
                               self.m.G(name + ".weight"), self.m.G(name + ".bias"), add1=add1, add2=add2, out=out)
 
-    def bn_bwd_split(self, name, dz, x, relu):
+    def bn_bwd_split(self, name, dz, x, relu, part=None):
         sc, sh, mu, istd = self.bnc(name)
-        return Kn.bn_backward_split(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.part,
+        return Kn.bn_backward_split(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, part,
                                     self._coef(), self.m.G(name + ".weight"), self.m.G(name + ".bias"), 3, 1)
 
     def wgrad(self, name, dy, x, KS, stride=1, pro=None):
