@@ -88,12 +88,12 @@ class ConvTimer:
     def __enter__(self):
         orig, orig_psa = self.orig, self.orig_psa
 
-        def wrapped_psa(xs, ws, bias, res=None, out=None, stat_part=None):
+        def wrapped_psa(xs, ws, bias, res=None, out=None, stat_part=None, bwd=None):
             if not self.active or ws.shape[1] != 9 or bias is None:
-                return orig_psa(xs, ws, bias, res, out, stat_part)
+                return orig_psa(xs, ws, bias, res, out, stat_part, bwd)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            y = orig_psa(xs, ws, bias, res, out, stat_part)
+            y = orig_psa(xs, ws, bias, res, out, stat_part, bwd)
             e.record()
             self.events.append((s, e))
             self.kind = "psa"

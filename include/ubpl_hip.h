@@ -208,7 +208,12 @@ int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, int Cin, in
                              const float* pshift, float* slab, float* dw, float* db, int accumulate, void* stream);
 int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                             const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
-                            const float* res, float* y, float* slab, int npieces, float* stat_part, void* stream);
+                            const float* res, float* y, float* slab, int npieces, float* stat_part,
+                            const float* bn_x, const float* bn_coef, int bn_relu, float* bn_part, void* stream);
+/* bn_part (nullable; with bn_x [B,Cout,P], bn_coef = scale|shift|mean, Cout
+ * floats each, bn_relu): when y is the data gradient dz of a BatchNorm(+ReLU)
+ * with input bn_x, its backward statistics partials (ubpl_bn_backward layout),
+ * from the epilogue — then ubpl_bn_backward(..., part_ready = 1) needs no pass. */
 /* 1x1 stride-1 conv on the 6xbf16 path with the f32 activations split while
  * they are staged (no pre-split image): y = conv(relu(x*pscale + pshift) or x)
  * + bias (+ res, may alias y); wsplit = 3 planes of [Cout][Cin] from
@@ -218,7 +223,8 @@ int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, 
 int ubpl_conv1x1_split_load_preferred(int B, int Cin, int Cout, int P);
 int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int P, const uint16_t* wsplit, int64_t wplane,
                                     const float* bias, int Cout, const float* pscale, const float* pshift,
-                                    const float* res, float* y, float* stat_part, void* stream);
+                                    const float* res, float* y, float* stat_part, const float* bn_x,
+                                    const float* bn_coef, int bn_relu, float* bn_part, void* stream);
 
 /* MaxPool2d(2,2) (models/base/layers.py:93), Upsample(x2, nearest) + add
  * (layers.py:110-111), AvgPool2d(2,2) projection (models/pose/hourglass.py:226). */

@@ -307,3 +307,35 @@ def test_wgrad1x1_split_load_vs_f64(case):
     print("wgrad1 %s: f32 %.2e split-load %.2e" % (case, e32, esp))
     assert esp <= 2 * e32 + 1e-8, (esp, e32)
     assert _rel(db + 0.5, dbref) <= 1e-5
+
+
+@pytest.mark.parametrize("kind", ["sol", "psa", "psa_splitk"])
+def test_bn_backward_partials_from_dgrad_epilogue(kind):
+    """Backward BatchNorm statistics partials written by the data-gradient
+    epilogue (conv1x1_sol_kernel / conv_psa_kernel, or the split-K fallback
+    pass) give the same dx, dgamma, dbeta as the statistics pass over dz."""
+    from ubpl_amd import kernels as Kn
+    gen = torch.Generator().manual_seed(23)
+    B, Ci, Co, H = {"sol": (2, 128, 256, 32), "psa": (2, 128, 128, 32), "psa_splitk": (4, 128, 128, 8)}[kind]
+    d = lambda t: t.to(DEV)
+    dy = d(torch.randn(B, Ci, H, H, generator=gen))
+    xbn = d(torch.randn(B, Co, H, H, generator=gen))
+    w = d(torch.randn(Ci, Co, 1 if kind == "sol" else 3, 1 if kind == "sol" else 3, generator=gen) * 0.05)
+    gamma = d(torch.rand(Co, generator=gen) + 0.5)
+    mean, istd = d(torch.randn(Co, generator=gen) * 0.1), d(torch.rand(Co, generator=gen) + 0.5)
+    coef = torch.cat([gamma * istd, d(torch.randn(Co, generator=gen)), mean])   # scale | shift | mean
+    sc, sh = coef[:Co], coef[Co:2 * Co]
+    part = Kn.bn_partial_buffer(Co, B * H * H, DEV)
+    if kind == "sol":
+        dz = Kn.conv1x1_forward_split_load(dy, Kn.conv_weight_split(w, 1, 3), None, bwd=(xbn, coef, 1, part))
+    else:
+        ys = Kn.split_activation(dy, 3, 1)
+        dz = Kn.conv2d_forward_psa(ys, Kn.conv_weight_split(w, 1, 3), None, bwd=(xbn, coef, 1, part))
+    res = []
+    for p in (part, None):
+        c3 = torch.empty(3 * Co, device=DEV)
+        dg, db = torch.zeros(Co, device=DEV), torch.zeros(Co, device=DEV)
+        dx = Kn.bn_backward(dz, xbn, gamma, mean, istd, sc, sh, 1, p, c3, dg, db, out=torch.empty_like(dz))
+        res.append((dx, dg, db))
+    for a, b in zip(*res):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)

@@ -225,4 +225,51 @@ __device__ __forceinline__ void tile_bn_partials(const ACC (&acc)[TM][TN], const
     }
 }
 
+// BatchNorm BACKWARD partials of a data-gradient tile (the conv output is dz
+// of the BN whose input is x): per channel m and 64-pixel slice q,
+// (S1, S2) = (sum g, sum g*(x - mean)), g = dz under the recomputed ReLU mask
+// — bn.hip bn_bwd_partials_kernel's layout and formula, from the accumulators
+// (no dz re-read; x is read at the tile's own addresses).
+struct BnBwdEpi {
+    const float* x;      // BN input [B][M][P] (nullptr: off)
+    const float* coef;   // scale | shift | mean, M floats each
+    int relu;
+    float* part;         // [M][ceil(N/64)][2]
+};
+
+template <int TM, int TN, typename ACC>
+__device__ __forceinline__ void tile_bn_bwd_partials(const ACC (&acc)[TM][TN], const bool (&nok)[TN],
+                                                     const int64_t (&obase)[TN], int mrow0, int M, int P,
+                                                     int64_t nwave0, int64_t N, const BnBwdEpi& e) {
+    static_assert(TN % 2 == 0, "a wave covers whole 64-pixel slices (2 fragments of 32 each)");
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int64_t np = (N + 63) / 64;
+#pragma unroll
+    for (int sp = 0; sp < TN / 2; ++sp) {
+        const int64_t ns0 = nwave0 + 64 * sp;
+        if (ns0 >= N) break;
+        const int64_t q = ns0 / 64;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int mc = m < M ? m : M - 1;
+                const float sc = e.coef[mc], sh = e.coef[M + mc], mu = e.coef[2 * M + mc];
+                const float x0 = e.x[obase[2 * sp] + (int64_t)mc * P];
+                const float x1 = e.x[obase[2 * sp + 1] + (int64_t)mc * P];
+                float g0 = nok[2 * sp] ? acc[i][2 * sp][r] : 0.f;
+                float g1 = nok[2 * sp + 1] ? acc[i][2 * sp + 1][r] : 0.f;
+                if (e.relu && !(fmaf(x0, sc, sh) > 0.f)) g0 = 0.f;
+                if (e.relu && !(fmaf(x1, sc, sh) > 0.f)) g1 = 0.f;
+                const float s1 = half_sum_dpp(g0 + g1);
+                const float s2 = half_sum_dpp(fmaf(g0, x0 - mu, g1 * (x1 - mu)));
+                if ((lane & 31) == 31 && m < M) {
+                    e.part[((int64_t)m * np + q) * 2] = s1;
+                    e.part[((int64_t)m * np + q) * 2 + 1] = s2;
+                }
+            }
+    }
+}
+
 }  // namespace ubpl

@@ -333,7 +333,8 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
                                                         int B, int Cin, int H, int W, int pad, int Cout, int kchunk,
-                                                        float* __restrict__ slab, float* __restrict__ stat_part) {
+                                                        float* __restrict__ slab, float* __restrict__ stat_part,
+                                                        ubpl::BnBwdEpi bwd) {
     constexpr int PADK = (KS - 1) / 2;
     constexpr int T = KS * KS;
     // waves: WGM along the output channels x 4/WGM along the pixels (64-row
@@ -506,6 +507,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
         return;
     }
     if (stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0 + wm, Cout, n0 + wn, N, stat_part);
+    if (bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, n0 + wn, N, bwd);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         if (!nok[j]) continue;
@@ -539,7 +541,7 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
                                                            const float* __restrict__ pscale,
                                                            const float* __restrict__ pshift, const float* res,
                                                            float* y, int B, int K, int P, int M,
-                                                           float* __restrict__ stat_part) {
+                                                           float* __restrict__ stat_part, ubpl::BnBwdEpi bwd) {
     constexpr int NP = 3, BNT = 256, NS = 2;
     constexpr int TM = BM / 32, TN = 2;
     constexpr int AB = NP * BM * 32;         // A stage bytes: [piece][BM rows][32 B]
@@ -671,6 +673,7 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
     }
 
     if (stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0, M, n0 + wn, N, stat_part);
+    if (bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0, M, P, n0 + wn, N, bwd);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         if (!nok[j]) continue;
@@ -1161,18 +1164,25 @@ void launch_split_reduce(const float* slab, int splits, int Cout, int P, int64_t
 template <int BM, int KS, int NP, int BNT, int WGM = 2>
 int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t wplane, const float* bias,
                const float* res, float* y, int B, int Cin, int H, int W, int pad, int Cout, const Plan& pl,
-               float* slab, float* stat_part, hipStream_t st) {
+               float* slab, float* stat_part, const ubpl::BnBwdEpi& bwd, hipStream_t st) {
     const int64_t N = (int64_t)B * H * W;
     dim3 grid((unsigned)((N + BNT - 1) / BNT), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
     const bool split = pl.splits > 1;
+    const ubpl::BnBwdEpi off{nullptr, nullptr, 0, nullptr};
     hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM>), grid, dim3(NT), 0, st, xs, xplane, wp, wplane, bias,
                        split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr,
-                       split ? nullptr : stat_part);
+                       split ? nullptr : stat_part, split ? off : bwd);
     UBPL_LAUNCH_CHECK();
     if (split) {
         launch_split_reduce(slab, pl.splits, Cout, H * W, N, bias, res, y, st);
         UBPL_LAUNCH_CHECK();
-        if (stat_part) return ubpl_bn_partials(y, B, Cout, H * W, stat_part, st);
+        if (stat_part) {
+            const int e = ubpl_bn_partials(y, B, Cout, H * W, stat_part, st);
+            if (e) return e;
+        }
+        if (bwd.part)
+            return ubpl_bn_backward_partials(y, bwd.x, B, Cout, H * W, bwd.coef, bwd.coef + Cout,
+                                             bwd.coef + 2 * Cout, bwd.relu, bwd.part, st);
     }
     return 0;
 }
@@ -1332,9 +1342,11 @@ UBPL_API int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int
 UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                                      const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
                                      const float* res, float* y, float* slab, int npieces, float* stat_part,
+                                     const float* bn_x, const float* bn_coef, int bn_relu, float* bn_part,
                                      void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (Cin % 16 != 0 || (npieces != 2 && npieces != 3) || pad < (KS - 1) / 2) return (int)hipErrorInvalidValue;
+    const ubpl::BnBwdEpi bwd{bn_part ? bn_x : nullptr, bn_coef, bn_relu, bn_part};
     if ((((uintptr_t)wsplit) & 15) != 0 || (((uintptr_t)xs) & 15) != 0 || (wplane % 8) != 0 || (xplane % 8) != 0)
         return (int)hipErrorInvalidValue;
     const int64_t N = (int64_t)B * H * W;
@@ -1355,17 +1367,17 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     }();
     if (bm64w && pl.bm == 64 && pl.splits == 1 && npieces == 3 && KS == 3 && N % 256 == 0)
         return launch_psa<64, 3, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                            slab, stat_part, st);
+                                            slab, stat_part, bwd, st);
     if (bn256 && pl.bm == 128 && pl.splits == 1 && npieces == 3 && N % 256 == 0) {
         if (KS == 3)
             return launch_psa<128, 3, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                              slab, stat_part, st);
+                                              slab, stat_part, bwd, st);
         return launch_psa<128, 1, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                          slab, stat_part, st);
+                                          slab, stat_part, bwd, st);
     }
 #define UBPL_PS(BM_, KS_, NP_) \
     return launch_psa<BM_, KS_, NP_, 128>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl, \
-                                          slab, stat_part, st)
+                                          slab, stat_part, bwd, st)
 #define UBPL_PS_BM(KS_, NP_)          \
     if (pl.bm == 128) UBPL_PS(128, KS_, NP_); \
     UBPL_PS(64, KS_, NP_)
@@ -1408,6 +1420,7 @@ UBPL_API int ubpl_conv1x1_split_load_preferred(int B, int Cin, int Cout, int P) 
 UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int P, const uint16_t* wsplit,
                                              int64_t wplane, const float* bias, int Cout, const float* pscale,
                                              const float* pshift, const float* res, float* y, float* stat_part,
+                                             const float* bn_x, const float* bn_coef, int bn_relu, float* bn_part,
                                              void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (!sol_supported(B, Cin, Cout, P) || (((uintptr_t)x) & 15) || (((uintptr_t)wsplit) & 15) || (wplane % 8))
@@ -1415,10 +1428,11 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     const bool pro = pscale != nullptr;
     const int64_t N = (int64_t)B * P;
     const int bm = Cout % 128 == 0 ? 128 : 64;
+    const ubpl::BnBwdEpi bwd{bn_part ? bn_x : nullptr, bn_coef, bn_relu, bn_part};
     dim3 grid((unsigned)((N + 255) / 256), (unsigned)(Cout / bm));
 #define UBPL_SOL(BM_, PRO_)                                                                                       \
     hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_>), grid, dim3(NT), 0, st, x, wsplit, wplane, bias, pscale, \
-                       pshift, res, y, B, Cin, P, Cout, stat_part)
+                       pshift, res, y, B, Cin, P, Cout, stat_part, bwd)
     if (bm == 128) {
         if (pro) UBPL_SOL(128, true);
         else UBPL_SOL(128, false);

@@ -58,9 +58,9 @@ SIGNATURES = {
     "ubpl_conv_weights_split": (I, [P, P, L, P, I, I, I, P]),
     "ubpl_split_activation": (I, [P, I, I, I, I, P, P, I, I, P, L, P]),
     "ubpl_conv2d_forward_psa_workspace": (L, [I, I, I, I, I, I, I]),
-    "ubpl_conv2d_forward_psa": (I, [P, L, I, I, I, I, I, P, L, P, I, I, P, P, P, I, P, P]),
+    "ubpl_conv2d_forward_psa": (I, [P, L, I, I, I, I, I, P, L, P, I, I, P, P, P, I, P, P, P, I, P, P]),
     "ubpl_conv1x1_split_load_preferred": (I, [I, I, I, I]),
-    "ubpl_conv1x1_forward_split_load": (I, [P, I, I, I, P, L, P, I, P, P, P, P, P, P]),
+    "ubpl_conv1x1_forward_split_load": (I, [P, I, I, I, P, L, P, I, P, P, P, P, P, P, P, I, P, P]),
     "ubpl_maxpool2x2_forward": (I, [P, L, I, I, P, P]),
     "ubpl_maxpool2x2_backward": (I, [P, P, L, I, I, P, I, P]),
     "ubpl_avgpool2x2_forward": (I, [P, L, I, I, P, P]),

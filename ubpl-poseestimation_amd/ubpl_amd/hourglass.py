@@ -36,6 +36,10 @@ _PRODUCER_STATS = os.environ.get("UBPL_PRODUCER_STATS", "1") != "0"
 _WGRAD3_64 = os.environ.get("UBPL_WGRAD3_64", "1") != "0"
 # 1x1 weight gradients on the 6xbf16 split-on-load kernel (UBPL_WGRAD1_SPLIT=0: exact-f32 kernel)
 _WGRAD1_SPLIT = os.environ.get("UBPL_WGRAD1_SPLIT", "1") != "0"
+# BatchNorm backward statistics from the data-gradient epilogues (UBPL_BWD_EPI=1).  Off by
+# default: the epilogue's x reads sit on the critical path of the big dgrad launches and
+# cost more (-3 % step) than the separate streaming partials pass they replace.
+_BWD_EPI = os.environ.get("UBPL_BWD_EPI", "0") == "1"
 
 
 # ---------------------------------------------------------------------------
@@ -598,12 +602,26 @@ class _Exec:
         Kn.conv2d_wgrad(dy, x, KS, stride, self.m.G(name + ".weight"), self.m.G(name + ".bias"), ps, ph,
                         accumulate=True)
 
-    def dgrad(self, name, dy, res=None, out=None):
+    def bwd_epi(self, bn, x):
+        """(bwd argument, partials buffer): the data-gradient epilogue writes the
+        backward statistics partials of BN `bn` (input x) — None off the path."""
+        if not self.train or bn is None or not _BWD_EPI:
+            return None, None
+        part = Kn.bn_partial_buffer(x.shape[1], x.shape[0] * x[0, 0].numel(), x.device)
+        return (x, self.bnc(bn)[0], 1, part), part
+
+    def dgrad(self, name, dy, res=None, out=None, bnb=None):
+        """bnb = (bn, x): the result is dz of BN bn (input x) — returns (dx, its
+        backward partials or None); else dx."""
         ws = self.m.SW(1, name + ".weight")
         if ws is not None and ws.npieces == 3 and ws.shape[1] == 1:
             if Kn.conv1x1_split_load_ok(dy, ws):
-                return Kn.conv1x1_forward_split_load(dy, ws, None, res=res, out=out)
+                bwd, part = self.bwd_epi(*(bnb or (None, None)))
+                y = Kn.conv1x1_forward_split_load(dy, ws, None, res=res, out=out, bwd=bwd)
+                return (y, part) if bnb is not None else y
             ws = None
+        if bnb is not None:
+            return self.dgrad(name, dy, res=res, out=out), None
         if ws is not None:
             if ws.npieces == 3:
                 ys = Kn.split_activation(dy, 3, (ws.shape[1] == 9) * 1)
@@ -622,33 +640,35 @@ class _Exec:
         c2 = self.bnc(p + ".bn2")[:2]
         c3 = self.bnc(p + ".bn3")[:2]
         self.wgrad(p + ".conv3.conv", dout, t2, 1, pro=c3)
-        d = self.dgrad(p + ".conv3.conv", dout)                       # d relu(bn3(t2))
+        d, part = self.dgrad(p + ".conv3.conv", dout, bnb=(p + ".bn3", t2))   # d relu(bn3(t2))
         ws = self.m.SW(1, p + ".conv2.conv.weight")
         xs = self.saved_split.get(p + ".conv2.conv")
         cb = 64 if _WGRAD3_64 else 128
         split_wgrad = (ws is not None and ws.npieces == 3 and xs is not None and t2.shape[1] % cb == 0
                        and xs.C % cb == 0 and t2.shape[3] % 16 == 0)
+        bwd2, part2 = self.bwd_epi(p + ".bn2", t1)
         if split_wgrad:
             # d t2 only as the split operand both conv2 gradients read
-            ys = self.bn_bwd_split(p + ".bn3", d, t2, relu=1)
+            ys = self.bn_bwd_split(p + ".bn3", d, t2, relu=1, part=part)
             Kn.conv2d_wgrad3_psa(ys, xs, self.m.G(p + ".conv2.conv.weight"), self.m.G(p + ".conv2.conv.bias"))
-            d = Kn.conv2d_forward_psa(ys, ws, None)                    # d relu(bn2(t1))
+            d = Kn.conv2d_forward_psa(ys, ws, None, bwd=bwd2)         # d relu(bn2(t1))
         elif ws is not None and ws.npieces == 3:
-            d = self.bn_bwd(p + ".bn3", d, t2, relu=1)                 # d t2
+            d = self.bn_bwd(p + ".bn3", d, t2, relu=1, part=part)     # d t2
             self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
-            d = Kn.conv2d_forward_psa(Kn.split_activation(d, 3, 1), ws, None)
+            d = Kn.conv2d_forward_psa(Kn.split_activation(d, 3, 1), ws, None, bwd=bwd2)
         else:
-            d = self.bn_bwd(p + ".bn3", d, t2, relu=1)                 # d t2
+            d = self.bn_bwd(p + ".bn3", d, t2, relu=1, part=part)     # d t2
             self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
             d = self.dgrad(p + ".conv2.conv", d)                       # d relu(bn2(t1))
-        d = self.bn_bwd(p + ".bn2", d, t1, relu=1)                     # d t1
+            part2 = None
+        d = self.bn_bwd(p + ".bn2", d, t1, relu=1, part=part2)        # d t1
         self.wgrad(p + ".conv1.conv", d, x, 1, pro=c1)
-        d = self.dgrad(p + ".conv1.conv", d)                           # d relu(bn1(x))
+        d, part = self.dgrad(p + ".conv1.conv", d, bnb=(p + ".bn1", x))   # d relu(bn1(x))
         if cin != cout:
             self.wgrad(p + ".skip_layer.conv", dout, x, 1)
             ds = self.dgrad(p + ".skip_layer.conv", dout)
-            return self.bn_bwd(p + ".bn1", d, x, relu=1, add1=ds)
-        return self.bn_bwd(p + ".bn1", d, x, relu=1, add1=dout)
+            return self.bn_bwd(p + ".bn1", d, x, relu=1, add1=ds, part=part)
+        return self.bn_bwd(p + ".bn1", d, x, relu=1, add1=dout, part=part)
 
     def hourglass_bwd(self, p, n, dout):
         x = self.saved.get(p)

@@ -471,9 +471,11 @@ def split_activation(x, npieces, pad, pscale=None, pshift=None, out=None):
     return SplitAct(out, plane, B, C, H, W, pad, npieces)
 
 
-def conv2d_forward_psa(xs, ws, bias, res=None, out=None, stat_part=None):
+def conv2d_forward_psa(xs, ws, bias, res=None, out=None, stat_part=None, bwd=None):
     """Stride-1 conv of pre-split activations xs (SplitAct) with SplitWeights ws;
-    stat_part: BatchNorm partials of the output (bn_partial_buffer)."""
+    stat_part: BatchNorm partials of the output (bn_partial_buffer); bwd =
+    (x, coef, relu, part): the output is dz of a BN with input x — its backward
+    statistics partials into part."""
     Cout, T, wc = ws.shape
     KS = int(round(T ** 0.5))
     if wc != xs.C or ws.npieces != xs.npieces:
@@ -483,7 +485,7 @@ def conv2d_forward_psa(xs, ws, bias, res=None, out=None, stat_part=None):
     nws = _lib.lib().ubpl_conv2d_forward_psa_workspace(B, xs.C, Cout, KS, H, W, ws.npieces)
     slab = torch.empty(int(nws), device=xs.buf.device, dtype=F32) if nws > 0 else None
     call("ubpl_conv2d_forward_psa", _p(xs.buf), int(xs.plane), B, xs.C, H, W, int(xs.pad), ws.ptr(), int(ws.plane),
-         _p(bias), Cout, KS, _p(res), _p(y), _p(slab), int(ws.npieces), _p(stat_part), stream())
+         _p(bias), Cout, KS, _p(res), _p(y), _p(slab), int(ws.npieces), _p(stat_part), *_bnb(bwd), stream())
     return y
 
 
@@ -495,7 +497,17 @@ def conv1x1_split_load_ok(x, ws):
             and bool(_lib.lib().ubpl_conv1x1_split_load_preferred(B, Cin, ws.shape[0], H * W)))
 
 
-def conv1x1_forward_split_load(x, ws, bias, pscale=None, pshift=None, res=None, out=None, stat_part=None):
+def _bnb(bwd):
+    """bwd = (x, coef, relu, part): backward BN partials from the epilogue (see
+    ubpl_conv2d_forward_psa); coef = scale|shift|mean (3*C contiguous floats)."""
+    if bwd is None:
+        return None, None, 0, None
+    x, coef, relu, part = bwd
+    return _p(x), _p(coef), int(relu), _p(part)
+
+
+def conv1x1_forward_split_load(x, ws, bias, pscale=None, pshift=None, res=None, out=None, stat_part=None,
+                               bwd=None):
     """1x1 stride-1 conv on the 6xbf16 path with x (NCHW f32) split while it is
     staged: y = conv(relu(x*pscale + pshift) or x, ws) + bias (+ res; res may
     alias out); ws = SplitWeights (rows, 1, Cin) — a forward (mode 0) or a data
@@ -507,7 +519,7 @@ def conv1x1_forward_split_load(x, ws, bias, pscale=None, pshift=None, res=None, 
             ws.shape, ws.npieces, Cin))
     y = torch.empty((B, Cout, H, W), device=x.device, dtype=F32) if out is None else out
     call("ubpl_conv1x1_forward_split_load", _p(x), B, Cin, H * W, ws.ptr(), int(ws.plane), _p(bias), Cout,
-         _p(pscale), _p(pshift), _p(res), _p(y), _p(stat_part), stream())
+         _p(pscale), _p(pshift), _p(res), _p(y), _p(stat_part), *_bnb(bwd), stream())
     return y
 
 
