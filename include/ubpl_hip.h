@@ -111,20 +111,22 @@ int ubpl_bn_stats_from_partials(const float* part, int C, int64_t N, const float
                                 const float* beta, float eps, float momentum, float* rmean, float* rvar,
                                 float* mean_out, float* invstd_out, float* scale, float* shift_out, void* stream);
 /* Backward of y = [relu](bn(x)); dgamma/dbeta accumulate; dx = add1 + add2 + dL/dx.
- * part: ubpl_bn_partial_floats(C, B*HW) floats = per (channel, 64-pixel slice)
- * (S1, S2) = (sum g, sum g*(x - mean)), g = dz under the recomputed ReLU mask;
- * part_ready = 1: dz's producer already wrote them (a conv epilogue's bn_part
- * argument) and no statistics pass runs; coef: 3*C floats of scratch. */
+ * Statistics: one launch over `scratch` (ubpl_bn_part_doubles(B, C) doubles,
+ * zeroed before first use, as ubpl_bn_forward_stats), or — part != nullptr —
+ * from backward partials dz's producer wrote: per (channel, 64-pixel slice)
+ * (S1, S2) = (sum g, sum g*(x - mean)), g = dz under the recomputed ReLU mask,
+ * ubpl_bn_partial_floats(C, B*HW) floats (a conv epilogue's bn_part argument,
+ * or ubpl_bn_backward_partials); coef: 3*C floats of scratch. */
 int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma, const float* mean,
-                     const float* invstd, const float* scale, const float* shift, int relu, float* part,
-                     int part_ready, float* coef, float* dgamma, float* dbeta, const float* add1, const float* add2,
-                     float* dx, void* stream);
+                     const float* invstd, const float* scale, const float* shift, int relu, double* scratch,
+                     const float* part, float* coef, float* dgamma, float* dbeta, const float* add1,
+                     const float* add2, float* dx, void* stream);
 /* The same backward with dx delivered only as PSA planes (ubpl_split_activation
  * layout, border `pad`, npieces 2 or 3) — the operand of a split-path 3x3 data /
  * weight gradient; no addends; C % 16 == 0. */
 int ubpl_bn_backward_split(const float* dz, const float* x, int B, int C, int H, int W, const float* gamma,
                            const float* mean, const float* invstd, const float* scale, const float* shift, int relu,
-                           float* part, int part_ready, float* coef, float* dgamma, float* dbeta, int pad,
+                           double* scratch, const float* part, float* coef, float* dgamma, float* dbeta, int pad,
                            int npieces, uint16_t* dst, int64_t plane, void* stream);
 /* The backward statistics partials alone (the layout above). */
 int ubpl_bn_backward_partials(const float* dz, const float* x, int B, int C, int HW, const float* scale,

@@ -251,7 +251,7 @@ def test_bn_forward_backward_vs_torch():
         _close(rvd, rvr, rtol=1e-5, atol=1e-6)
         dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
         coef = torch.empty(3 * C, device=DEV)
-        dx = Kn.bn_backward(dz.to(DEV).clone(), xd, gam.to(DEV), mean, istd, sc, sh, 1, None, coef, dg, db)
+        dx = Kn.bn_backward(dz.to(DEV).clone(), xd, gam.to(DEV), mean, istd, sc, sh, 1, part, coef, dg, db)
         _close(dx, xr.grad, rtol=1e-4, atol=1e-5)
         _close(dg, gr.grad, rtol=1e-4, atol=1e-4)
         _close(db, br.grad, rtol=1e-4, atol=1e-4)

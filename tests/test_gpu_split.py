@@ -202,7 +202,8 @@ def test_bn_backward_split_matches_f32_then_split():
     gamma = d(torch.rand(C, generator=gen) + 0.5)
     mean, istd = d(torch.randn(C, generator=gen) * 0.1), d(torch.rand(C, generator=gen) + 0.5)
     sc, sh = gamma * istd, d(torch.randn(C, generator=gen)) - mean * gamma * istd
-    part = None                                  # statistics pass inside
+    part = torch.zeros(int(__import__("ubpl_amd")._lib.lib().ubpl_bn_part_doubles(B, C)), dtype=torch.float64,
+                       device=DEV)
     outs = []
     for mode in ("f32", "split"):
         coef = torch.empty(3 * C, device=DEV)
@@ -331,11 +332,14 @@ def test_bn_backward_partials_from_dgrad_epilogue(kind):
     else:
         ys = Kn.split_activation(dy, 3, 1)
         dz = Kn.conv2d_forward_psa(ys, Kn.conv_weight_split(w, 1, 3), None, bwd=(xbn, coef, 1, part))
+    scratch = torch.zeros(int(__import__("ubpl_amd")._lib.lib().ubpl_bn_part_doubles(B, Co)), dtype=torch.float64,
+                          device=DEV)
     res = []
     for p in (part, None):
         c3 = torch.empty(3 * Co, device=DEV)
         dg, db = torch.zeros(Co, device=DEV), torch.zeros(Co, device=DEV)
-        dx = Kn.bn_backward(dz, xbn, gamma, mean, istd, sc, sh, 1, p, c3, dg, db, out=torch.empty_like(dz))
+        dx = Kn.bn_backward(dz, xbn, gamma, mean, istd, sc, sh, 1, scratch, c3, dg, db, out=torch.empty_like(dz),
+                            part=p)
         res.append((dx, dg, db))
     for a, b in zip(*res):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)

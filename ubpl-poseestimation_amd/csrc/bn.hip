@@ -182,14 +182,74 @@ struct BwdOut {
     float *dgamma, *dbeta, *ca, *cb, *cc;
 };
 
-// Backward statistics, per (channel c, 64-pixel slice q of the flat (b, p)
-// range): part[(c*np + q)*2 + {0,1}] = (S1, S2) = (sum g, sum g*(x - mean)),
-// g = dz with the ReLU mask recomputed.  Plain stores, no atomics: the
-// channel's totals come from bn_bwd_finalize_kernel (a last-arriver hand-off
-// through memory-side atomics cost ~10 % of the training step).  One wave per
-// 4 slices of one channel: lane l takes pixels 4l..4l+3 (float4; P % 4 == 0),
-// a 16-lane row is one slice (DPP row sums).  The conv epilogues write the same
-// layout (common.h tile_bn_bwd_partials).
+// Per (channel, slice): S1 = sum dyp, S2 = sum dyp*(x - mean) with the ReLU
+// mask recomputed; the channel's last block produces dgamma/dbeta and the
+// coefficients of dx = a*dyp + b*(x - mean) + c.
+template <bool VEC>
+__global__ void __launch_bounds__(256) bwd_stats_kernel(const float* __restrict__ dz, const float* __restrict__ x,
+                                                       int B, int C, int HW, int bper,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float* __restrict__ mean, int relu,
+                                                       double* __restrict__ part, unsigned* __restrict__ cnt,
+                                                       BwdOut o) {
+    __shared__ double red[16];
+    const int c = blockIdx.x, sp = blockIdx.y;
+    const int b0 = sp * bper, b1 = min(B, b0 + bper);
+    const float sc = scale[c], sh = shift[c], mu = mean[c];
+    float s1 = 0.f, s2 = 0.f;
+    if (VEC) {
+        const int hw4 = HW >> 2;
+        const int n4 = (b1 - b0) * hw4;
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+        const float4* d4 = reinterpret_cast<const float4*>(dz);
+        for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+            const int bb = i / hw4, o4 = i - bb * hw4;
+            const int64_t off = ((int64_t)(b0 + bb) * C + c) * hw4 + o4;
+            const float4 xv = x4[off];
+            float4 g = d4[off];
+            if (relu) {
+                g.x = fmaf(xv.x, sc, sh) > 0.f ? g.x : 0.f;
+                g.y = fmaf(xv.y, sc, sh) > 0.f ? g.y : 0.f;
+                g.z = fmaf(xv.z, sc, sh) > 0.f ? g.z : 0.f;
+                g.w = fmaf(xv.w, sc, sh) > 0.f ? g.w : 0.f;
+            }
+            s1 += (g.x + g.y) + (g.z + g.w);
+            s2 = fmaf(g.x, xv.x - mu, fmaf(g.y, xv.y - mu, fmaf(g.z, xv.z - mu, fmaf(g.w, xv.w - mu, s2))));
+        }
+    } else {
+        const int n = (b1 - b0) * HW;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int bb = i / HW, o1 = i - bb * HW;
+            const int64_t off = ((int64_t)(b0 + bb) * C + c) * HW + o1;
+            const float xv = x[off];
+            float g = dz[off];
+            if (relu && !(fmaf(xv, sc, sh) > 0.f)) g = 0.f;
+            s1 += g;
+            s2 = fmaf(g, xv - mu, s2);
+        }
+    }
+    const double d1 = ubpl::block_sum((double)s1, red);
+    const double d2 = ubpl::block_sum((double)s2, red);
+    double t1, t2;
+    if (!combine_slices(part + (int64_t)c * gridDim.y * 2, sp, gridDim.y, cnt + c, d1, d2, t1, t2)) return;
+    const double N = (double)((int64_t)B * HW);
+    const double is = o.invstd[c], g = o.gamma[c];
+    if (o.dgamma) o.dgamma[c] += (float)(t2 * is);
+    if (o.dbeta) o.dbeta[c] += (float)t1;
+    o.ca[c] = (float)(g * is);
+    o.cb[c] = (float)(-g * is * is * is * t2 / N);
+    o.cc[c] = (float)(-g * is * t1 / N);
+}
+
+// Backward statistics partials, per (channel c, 64-pixel slice q of the flat
+// (b, p) range): part[(c*np + q)*2 + {0,1}] = (S1, S2) = (sum g, sum g*(x -
+// mean)), the layout the conv epilogues write (common.h tile_bn_bwd_partials),
+// combined by bn_bwd_finalize_kernel.  One wave per 4 x IT slices of one
+// channel: lane l takes pixels 4l..4l+3 of a 256-pixel chunk (float4; P % 4 ==
+// 0), a 16-lane row is one slice (DPP row sums).  (The default statistics path
+// is bwd_stats_kernel above — one launch; a partials pass + finalize launch
+// measured 0.7 % slower on the training step.)
 template <bool VEC>
 __global__ void __launch_bounds__(256) bn_bwd_partials_kernel(const float* __restrict__ dz,
                                                              const float* __restrict__ x, int C, int P, int64_t N,
@@ -564,26 +624,31 @@ __global__ void __launch_bounds__(256) bwd_apply_split_kernel(const float* __res
 }
 
 namespace {
-// statistics -> coefficients: the partials pass (unless the producer's
-// epilogue wrote them: part_ready), then the f64 finalize
+// statistics -> coefficients: one bwd_stats_kernel launch, or (part != nullptr:
+// the producer's epilogue wrote the partials) the f64 finalize
 int bwd_stats(const float* dz, const float* x, int B, int C, int HW, const float* gamma, const float* mean,
-              const float* invstd, const float* scale, const float* shift, int relu, float* part, int part_ready,
-              float* coef, float* dgamma, float* dbeta, hipStream_t st) {
+              const float* invstd, const float* scale, const float* shift, int relu, double* scratch,
+              const float* part, float* coef, float* dgamma, float* dbeta, hipStream_t st) {
+    const BwdOut o{gamma, invstd, dgamma, dbeta, coef, coef + C, coef + 2 * C};
+    if (part == nullptr) {   // one launch: slices + last-arriver combine
+        if (C > MAXBN || scratch == nullptr) return (int)hipErrorInvalidValue;
+        const int splits = splits_for(B, C);
+        const int bper = (B + splits - 1) / splits;
+        const int gs = (B + bper - 1) / bper;
+        const bool vec = (HW % 4 == 0) && ((((uintptr_t)dz | (uintptr_t)x) & 15) == 0);
+        unsigned* cnt = reinterpret_cast<unsigned*>(scratch);
+        double* sl = scratch + CNT_DOUBLES;
+        if (vec)
+            hipLaunchKernelGGL(bwd_stats_kernel<true>, dim3(C, gs), dim3(256), 0, st, dz, x, B, C, HW, bper, scale,
+                               shift, mean, relu, sl, cnt, o);
+        else
+            hipLaunchKernelGGL(bwd_stats_kernel<false>, dim3(C, gs), dim3(256), 0, st, dz, x, B, C, HW, bper, scale,
+                               shift, mean, relu, sl, cnt, o);
+        UBPL_LAUNCH_CHECK();
+        return 0;
+    }
     const int64_t N = (int64_t)B * HW;
     const int64_t np = (N + 63) / 64;
-    if (!part_ready) {
-        const bool vec = (HW % 4 == 0) && ((((uintptr_t)dz | (uintptr_t)x) & 15) == 0);
-        const int64_t waves = (int64_t)C * ((np + 15) / 16);
-        const dim3 grid((unsigned)((waves + 3) / 4));
-        if (vec)
-            hipLaunchKernelGGL(bn_bwd_partials_kernel<true>, grid, dim3(256), 0, st, dz, x, C, HW, N, scale, shift,
-                               mean, relu, part);
-        else
-            hipLaunchKernelGGL(bn_bwd_partials_kernel<false>, grid, dim3(256), 0, st, dz, x, C, HW, N, scale, shift,
-                               mean, relu, part);
-        UBPL_LAUNCH_CHECK();
-    }
-    const BwdOut o{gamma, invstd, dgamma, dbeta, coef, coef + C, coef + 2 * C};
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(FT), 0, st, part, np, N, o);
     UBPL_LAUNCH_CHECK();
     return 0;
@@ -591,7 +656,7 @@ int bwd_stats(const float* dz, const float* x, int B, int C, int HW, const float
 }  // namespace
 
 // Backward statistics partials of dz (ReLU mask from x's BN) alone: the layout
-// ubpl_bn_backward(..., part_ready = 1) takes; part: ubpl_bn_partial_floats(C, B*HW).
+// ubpl_bn_backward's `part` takes; part: ubpl_bn_partial_floats(C, B*HW) floats.
 UBPL_API int ubpl_bn_backward_partials(const float* dz, const float* x, int B, int C, int HW, const float* scale,
                                        const float* shift, const float* mean, int relu, float* part, void* stream) {
     const int64_t N = (int64_t)B * HW;
@@ -613,12 +678,12 @@ UBPL_API int ubpl_bn_backward_partials(const float* dz, const float* x, int B, i
 // addends): statistics, then bwd_apply_split_kernel.  C % 16 == 0.
 UBPL_API int ubpl_bn_backward_split(const float* dz, const float* x, int B, int C, int H, int W, const float* gamma,
                                     const float* mean, const float* invstd, const float* scale, const float* shift,
-                                    int relu, float* part, int part_ready, float* coef, float* dgamma, float* dbeta,
-                                    int pad, int npieces, uint16_t* dst, int64_t plane, void* stream) {
+                                    int relu, double* scratch, const float* part, float* coef, float* dgamma,
+                                    float* dbeta, int pad, int npieces, uint16_t* dst, int64_t plane, void* stream) {
     const int HW = H * W;
     if (C % 16 != 0 || npieces < 2 || npieces > 3 || pad < 0) return (int)hipErrorInvalidValue;
     hipStream_t st = (hipStream_t)stream;
-    const int e = bwd_stats(dz, x, B, C, HW, gamma, mean, invstd, scale, shift, relu, part, part_ready, coef, dgamma,
+    const int e = bwd_stats(dz, x, B, C, HW, gamma, mean, invstd, scale, shift, relu, scratch, part, coef, dgamma,
                             dbeta, st);
     if (e) return e;
     const float *ca = coef, *cb = coef + C, *cc = coef + 2 * C;
@@ -635,14 +700,15 @@ UBPL_API int ubpl_bn_backward_split(const float* dz, const float* x, int B, int 
 }
 
 // dx = BatchNorm(+ReLU) backward of dz (+ add1 + add2), dgamma/dbeta (+)= ;
-// part: ubpl_bn_partial_floats(C, B*HW) floats of scratch, or the backward
-// partials the producer of dz already wrote (part_ready = 1); coef: 3*C floats.
+// statistics by one bwd_stats_kernel launch over `scratch` (ubpl_bn_part_doubles,
+// zeroed before first use), or — part != nullptr — from the backward partials
+// dz's producer wrote (then only the f64 finalize runs); coef: 3*C floats.
 UBPL_API int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma,
                               const float* mean, const float* invstd, const float* scale, const float* shift,
-                              int relu, float* part, int part_ready, float* coef, float* dgamma, float* dbeta,
-                              const float* add1, const float* add2, float* dx, void* stream) {
+                              int relu, double* scratch, const float* part, float* coef, float* dgamma,
+                              float* dbeta, const float* add1, const float* add2, float* dx, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    const int e = bwd_stats(dz, x, B, C, HW, gamma, mean, invstd, scale, shift, relu, part, part_ready, coef, dgamma,
+    const int e = bwd_stats(dz, x, B, C, HW, gamma, mean, invstd, scale, shift, relu, scratch, part, coef, dgamma,
                             dbeta, st);
     if (e) return e;
     const uintptr_t al = (uintptr_t)dz | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)add1 | (uintptr_t)add2;

@@ -36,8 +36,8 @@ SIGNATURES = {
     "ubpl_bn_partial_floats": (L, [I, L]),
     "ubpl_bn_partials": (I, [P, I, I, I, P, P]),
     "ubpl_bn_stats_from_partials": (I, [P, I, L, P, P, F, F, P, P, P, P, P, P, P]),
-    "ubpl_bn_backward_split": (I, [P, P, I, I, I, I, P, P, P, P, P, I, P, I, P, P, P, I, I, P, L, P]),
-    "ubpl_bn_backward": (I, [P, P, I, I, I, P, P, P, P, P, I, P, I, P, P, P, P, P, P, P]),
+    "ubpl_bn_backward_split": (I, [P, P, I, I, I, I, P, P, P, P, P, I, P, P, P, P, P, I, I, P, L, P]),
+    "ubpl_bn_backward": (I, [P, P, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, P, P, P]),
     "ubpl_bn_backward_partials": (I, [P, P, I, I, I, P, P, P, I, P, P]),
     "ubpl_conv2d_forward": (I, [P, I, I, I, I, P, P, I, I, I, P, P, P, P, I, I, P, P]),
     "ubpl_conv2d_forward_workspace": (L, [I, I, I, I, I, I]),

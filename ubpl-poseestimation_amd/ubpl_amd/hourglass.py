@@ -30,8 +30,9 @@ from . import kernels as Kn
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 # residual bn1 statistics from the producer's partials (conv epilogue, max-pool,
-# upsample-add) instead of a pass over the input; UBPL_PRODUCER_STATS=0: the pass
-_PRODUCER_STATS = os.environ.get("UBPL_PRODUCER_STATS", "1") != "0"
+# upsample-add) instead of a pass over the input (UBPL_PRODUCER_STATS=1).  Off by
+# default: partials + a finalize launch lose to the one-launch pass (-0.6 % step).
+_PRODUCER_STATS = os.environ.get("UBPL_PRODUCER_STATS", "0") == "1"
 # 64-channel 3x3 weight gradients on the split path (UBPL_WGRAD3_64=0: exact-f32 kernel)
 _WGRAD3_64 = os.environ.get("UBPL_WGRAD3_64", "1") != "0"
 # 1x1 weight gradients on the 6xbf16 split-on-load kernel (UBPL_WGRAD1_SPLIT=0: exact-f32 kernel)
@@ -40,6 +41,10 @@ _WGRAD1_SPLIT = os.environ.get("UBPL_WGRAD1_SPLIT", "1") != "0"
 # default: the epilogue's x reads sit on the critical path of the big dgrad launches and
 # cost more (-3 % step) than the separate streaming partials pass they replace.
 _BWD_EPI = os.environ.get("UBPL_BWD_EPI", "0") == "1"
+# forward BatchNorm statistics from the conv epilogues (UBPL_FWD_EPI=1).  Off by default:
+# epilogue partials + a finalize launch measured 1.3 % slower than the one-launch
+# statistics pass (stats_kernel) on the training step.
+_FWD_EPI = os.environ.get("UBPL_FWD_EPI", "0") == "1"
 
 
 # ---------------------------------------------------------------------------
@@ -508,7 +513,8 @@ class _Exec:
         b = self.m.P(name + ".bias")
         ps, ph = (None, None) if pro is None else pro
         B, Cout = x.shape[0], w.shape[0]
-        mkpart = lambda: Kn.bn_partial_buffer(Cout, B * x.shape[2] * x.shape[3], x.device) if stats else None
+        mkpart = lambda: (Kn.bn_partial_buffer(Cout, B * x.shape[2] * x.shape[3], x.device)
+                          if stats and _FWD_EPI else None)
         ws = self.m.SW(0, name + ".weight") if stride == 1 else None
         if ws is not None and ws.npieces == 3 and ws.shape[1] == 1:
             if Kn.conv1x1_split_load_ok(x, ws):
@@ -585,13 +591,15 @@ class _Exec:
     def bn_bwd(self, name, dz, x, relu, add1=None, add2=None, out=None, part=None):
         """part: the backward partials dz's producer wrote (None: a statistics pass)."""
         sc, sh, mu, istd = self.bnc(name)
-        return Kn.bn_backward(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, part, self._coef(),
-                              self.m.G(name + ".weight"), self.m.G(name + ".bias"), add1=add1, add2=add2, out=out)
+        return Kn.bn_backward(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.part, self._coef(),
+                              self.m.G(name + ".weight"), self.m.G(name + ".bias"), add1=add1, add2=add2, out=out,
+                              part=part)
 
     def bn_bwd_split(self, name, dz, x, relu, part=None):
         sc, sh, mu, istd = self.bnc(name)
-        return Kn.bn_backward_split(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, part,
-                                    self._coef(), self.m.G(name + ".weight"), self.m.G(name + ".bias"), 3, 1)
+        return Kn.bn_backward_split(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.part,
+                                    self._coef(), self.m.G(name + ".weight"), self.m.G(name + ".bias"), 3, 1,
+                                    part=part)
 
     def wgrad(self, name, dy, x, KS, stride=1, pro=None):
         ps, ph = (None, None) if pro is None else pro

@@ -242,36 +242,28 @@ def bn_stats_from_partials(part, C, N, gamma, beta, eps, momentum, rmean, rvar, 
          _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift_out), stream())
 
 
-def _bwd_part(x, part):
-    """(buffer, ready): the producer's backward partials, or fresh scratch."""
-    if part is not None:
-        return part, 1
-    B, C = x.shape[:2]
-    return bn_partial_buffer(C, B * x[0, 0].numel(), x.device), 0
-
-
-def bn_backward_split(dz, x, gamma, mean, invstd, scale, shift, relu, part, coef, dgamma, dbeta, npieces, pad):
-    """bn_backward with dx delivered as a SplitAct (PSA planes) only.  part: the
-    backward partials dz's producer wrote (bn_bwd_partials layout) or None."""
+def bn_backward_split(dz, x, gamma, mean, invstd, scale, shift, relu, scratch, coef, dgamma, dbeta, npieces, pad,
+                      part=None):
+    """bn_backward with dx delivered as a SplitAct (PSA planes) only."""
     B, C, H, W = x.shape
     plane = B * C * (H + 2 * pad) * (W + 2 * pad)
     out = torch.empty(npieces * plane, device=x.device, dtype=torch.int16)
-    pbuf, ready = _bwd_part(x, part)
     call("ubpl_bn_backward_split", _p(dz), _p(x), B, C, H, W, _p(gamma), _p(mean), _p(invstd), _p(scale), _p(shift),
-         int(relu), _p(pbuf), ready, _p(coef), _p(dgamma), _p(dbeta), int(pad), int(npieces), _p(out), int(plane),
-         stream())
+         int(relu), _p(scratch), _p(part), _p(coef), _p(dgamma), _p(dbeta), int(pad), int(npieces), _p(out),
+         int(plane), stream())
     return SplitAct(out, plane, B, C, H, W, pad, npieces)
 
 
-def bn_backward(dz, x, gamma, mean, invstd, scale, shift, relu, part, coef, dgamma, dbeta, add1=None, add2=None,
-                out=None):
-    """BatchNorm(+ReLU) backward; part: the backward partials dz's producer wrote, or None."""
+def bn_backward(dz, x, gamma, mean, invstd, scale, shift, relu, scratch, coef, dgamma, dbeta, add1=None, add2=None,
+                out=None, part=None):
+    """BatchNorm(+ReLU) backward.  scratch: bn_part(B, C) (zeroed double
+    scratch of the one-launch statistics); part: the backward partials dz's
+    producer wrote (bn_bwd_partials layout) — then only the finalize runs."""
     B, C = x.shape[:2]
     HW = x[0, 0].numel()
     dx = dz if out is None else out
-    pbuf, ready = _bwd_part(x, part)
     call("ubpl_bn_backward", _p(dz), _p(x), B, C, HW, _p(gamma), _p(mean), _p(invstd), _p(scale), _p(shift),
-         int(relu), _p(pbuf), ready, _p(coef), _p(dgamma), _p(dbeta), _p(add1), _p(add2), _p(dx), stream())
+         int(relu), _p(scratch), _p(part), _p(coef), _p(dgamma), _p(dbeta), _p(add1), _p(add2), _p(dx), stream())
     return dx
 
 
