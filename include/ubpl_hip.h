@@ -216,6 +216,14 @@ int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, 
  * floats each, bn_relu): when y is the data gradient dz of a BatchNorm(+ReLU)
  * with input bn_x, its backward statistics partials (ubpl_bn_backward layout),
  * from the epilogue — then ubpl_bn_backward(..., part_ready = 1) needs no pass. */
+/* The 7x7 stride-2 stem (Cin <= 4) on the split path by space-to-depth: the
+ * phase images of x as a 16-channel PSA image with a `pad` (>= 2) border, and
+ * the equivalent 4x4 stride-1 weights (Cin' = 16, KS' = 4) split into npieces
+ * (= 3) planes of Cout*256 bf16; then ubpl_conv2d_forward_psa(..., KS = 4). */
+int ubpl_stem_s2d_split(const float* x, int B, int C, int H, int W, int pad, int npieces, uint16_t* dst,
+                        int64_t plane, void* stream);
+int ubpl_stem_weight_s2d_split(const float* w, int Cout, int C, int KS, int npieces, uint16_t* dst, int64_t plane,
+                               void* stream);
 /* 1x1 stride-1 conv on the 6xbf16 path with the f32 activations split while
  * they are staged (no pre-split image): y = conv(relu(x*pscale + pshift) or x)
  * + bias (+ res, may alias y); wsplit = 3 planes of [Cout][Cin] from

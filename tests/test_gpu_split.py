@@ -343,3 +343,24 @@ def test_bn_backward_partials_from_dgrad_epilogue(kind):
         res.append((dx, dg, db))
     for a, b in zip(*res):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("B,H", [(2, 64), (3, 32), (1, 256)])
+def test_stem_s2d_vs_f64(B, H):
+    """The 7x7 stride-2 stem as a 4x4 stride-1 conv over the space-to-depth
+    image on the split path, within 2x the exact-f32 kernel's error."""
+    from ubpl_amd import kernels as Kn
+    gen = torch.Generator().manual_seed(31 + B + H)
+    x = torch.rand(B, 3, H, H, generator=gen) - 0.5
+    w = torch.randn(64, 3, 7, 7, generator=gen) / np.sqrt(147)
+    b = torch.randn(64, generator=gen)
+    yref = F.conv2d(x.double(), w.double(), b.double(), 2, 3)
+    d = lambda t: t.to(DEV)
+    assert Kn.stem_s2d_ok(d(x))
+    y = Kn.conv2d_forward_psa(Kn.stem_s2d_split(d(x), 2), Kn.stem_weight_s2d_split(d(w)), d(b))
+    y32 = Kn.conv2d_forward(d(x), d(w), d(b), 2)
+    e32, esp = _rel(y32, yref), _rel(y, yref)
+    print("stem s2d B=%d H=%d: f32 %.2e split %.2e" % (B, H, e32, esp))
+    # K = 147 keeps the exact-f32 chain below one f32 ulp (~4e-8 relative); the
+    # split path rounds once per 16-term chunk (16 chunks): a few ulps is its level
+    assert esp <= max(2 * e32, 4 * 2.0 ** -24), (esp, e32)

@@ -309,6 +309,65 @@ __global__ void __launch_bounds__(256) split_act_kernel(const float* __restrict_
     ubpl::store_psa_row<NP>(v, dst + (((int64_t)(b * G + g) * Hp + hp) * Wp + wq) * 16, plane);
 }
 
+// ------------------------------------------------------------------ the stem on the split path
+// Space-to-depth: the 7x7 stride-2 pad-3 stem conv (models/pose/hourglass.py
+// pre.0, models/base/layers.py:31-50) = a stride-1 4x4 conv over the 4 phase
+// images x'[c*4 + 2ph + pw][i][j] = x[c][2i + ph][2j + pw] with taps
+// (a, b) in 0..3 at offsets (a - 2, b - 2) and the kernel
+// w'[o][c*4 + 2ph + pw][a][b] = w[o][c][2(a - 2) + ph + 3][2(b - 2) + pw + 3]
+// (zero outside the 7x7 window): K = 16 channels x 16 taps on the split path
+// instead of 147 on the exact-f32 kernel.  The phase image goes straight to the
+// PSA layout (C*4 <= 16 channels, the rest zero) with a `pad` border.
+template <int NP>
+__global__ void __launch_bounds__(256) stem_s2d_split_kernel(const float* __restrict__ x, int C, int H, int W,
+                                                            int pad, uint16_t* __restrict__ dst, int64_t plane) {
+    const int Ho = H / 2, Wo = W / 2;
+    const int Hp = Ho + 2 * pad, Wp = Wo + 2 * pad;
+    const int b = blockIdx.y;
+    const int pix = blockIdx.x * 256 + threadIdx.x;
+    if (pix >= Hp * Wp) return;
+    const int hp = pix / Wp, wq = pix - hp * Wp;
+    const int i = hp - pad, j = wq - pad;
+    const bool in = i >= 0 && i < Ho && j >= 0 && j < Wo;
+    float v[16];
+#pragma unroll
+    for (int ch = 0; ch < 16; ++ch) {
+        const int c = ch >> 2, ph = (ch >> 1) & 1, pw = ch & 1;
+        const bool ok = in && c < C;
+        const int64_t off = (((int64_t)b * C + (ok ? c : 0)) * H + (ok ? 2 * i + ph : 0)) * W + (ok ? 2 * j + pw : 0);
+        const float t = x[off];
+        v[ch] = ok ? t : 0.f;
+    }
+    ubpl::store_psa_row<NP>(v, dst + (((int64_t)b * Hp + hp) * Wp + wq) * 16, plane);
+}
+
+// w [Cout][C][KS][KS] (KS odd, stride 2, pad KS/2) -> the split, grouped
+// tap-major weights of the s2d conv: [piece][Cout][KT*KT taps][16 channels]
+// (KT = 4 for KS = 7): tap (a, b) of phase (ph, pw) is w[.][.][2(a - KT/2) +
+// ph + KS/2][2(b - KT/2) + pw + KS/2], zero outside the KSxKS window.
+template <int NP>
+__global__ void __launch_bounds__(256) stem_weight_s2d_split_kernel(const float* __restrict__ w, int Cout, int C,
+                                                                   int KS, int KT, uint16_t* __restrict__ dst,
+                                                                   int64_t plane) {
+    const int64_t total = (int64_t)Cout * KT * KT * 16;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int ch = (int)(idx % 16);
+    const int tap = (int)((idx / 16) % (KT * KT));
+    const int o = (int)(idx / (16 * KT * KT));
+    const int a = tap / KT, bb = tap - a * KT;
+    const int c = ch >> 2, ph = (ch >> 1) & 1, pw = ch & 1;
+    const int kh = 2 * (a - KT / 2) + ph + KS / 2, kw = 2 * (bb - KT / 2) + pw + KS / 2;
+    const bool ok = c < C && kh >= 0 && kh < KS && kw >= 0 && kw < KS;
+    float v = ok ? w[(((int64_t)o * C + c) * KS + kh) * KS + kw] : 0.f;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const __bf16 hv = (__bf16)v;
+        dst[(int64_t)p * plane + idx] = __builtin_bit_cast(uint16_t, hv);
+        v -= (float)hv;
+    }
+}
+
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
@@ -335,7 +394,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                                                         int B, int Cin, int H, int W, int pad, int Cout, int kchunk,
                                                         float* __restrict__ slab, float* __restrict__ stat_part,
                                                         ubpl::BnBwdEpi bwd) {
-    constexpr int PADK = (KS - 1) / 2;
+    constexpr int PADK = KS / 2;   // odd KS: centred; even KS (the stem, 4x4): taps -KS/2 .. KS/2 - 1
     constexpr int T = KS * KS;
     // waves: WGM along the output channels x 4/WGM along the pixels (64-row
     // tiles on 256 pixels: 1 x 4, wave tile 64 x 64)
@@ -1345,7 +1404,8 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
                                      const float* bn_x, const float* bn_coef, int bn_relu, float* bn_part,
                                      void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    if (Cin % 16 != 0 || (npieces != 2 && npieces != 3) || pad < (KS - 1) / 2) return (int)hipErrorInvalidValue;
+    if (Cin % 16 != 0 || (npieces != 2 && npieces != 3) || pad < KS / 2 || (KS != 1 && KS != 3 && KS != 4))
+        return (int)hipErrorInvalidValue;
     const ubpl::BnBwdEpi bwd{bn_part ? bn_x : nullptr, bn_coef, bn_relu, bn_part};
     if ((((uintptr_t)wsplit) & 15) != 0 || (((uintptr_t)xs) & 15) != 0 || (wplane % 8) != 0 || (xplane % 8) != 0)
         return (int)hipErrorInvalidValue;
@@ -1365,6 +1425,11 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         const char* e = getenv("UBPL_PSA_BM64W");
         return !(e && atoi(e) == 0);
     }();
+    if (KS == 4) {   // the space-to-depth stem (ubpl_stem_s2d_split): 64-row tiles on 256 pixels
+        if (pl.bm != 64 || pl.splits != 1 || npieces != 3 || N % 256 != 0) return (int)hipErrorInvalidValue;
+        return launch_psa<64, 4, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
+                                            slab, stat_part, bwd, st);
+    }
     if (bm64w && pl.bm == 64 && pl.splits == 1 && npieces == 3 && KS == 3 && N % 256 == 0)
         return launch_psa<64, 3, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                             slab, stat_part, bwd, st);
@@ -1540,4 +1605,32 @@ UBPL_API int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, in
                            per, slab);
     UBPL_LAUNCH_CHECK();
     return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 1, db != nullptr, dw, db, accumulate, stream);
+}
+
+// ---- the stem on the split path (space-to-depth, see stem_s2d_split_kernel)
+// x [B][C][H][W] (C <= 4, H, W even) -> PSA planes [B][1][H/2 + 2pad][W/2 + 2pad][16]
+// of the 4 phase images per channel; pad >= 2 for the 7x7 stem.
+UBPL_API int ubpl_stem_s2d_split(const float* x, int B, int C, int H, int W, int pad, int npieces, uint16_t* dst,
+                                 int64_t plane, void* stream) {
+    if (C < 1 || C > 4 || (H & 1) || (W & 1) || npieces != 3 || pad < 0 || (plane % 8) != 0)
+        return (int)hipErrorInvalidValue;
+    const int Hp = H / 2 + 2 * pad, Wp = W / 2 + 2 * pad;
+    dim3 grid((unsigned)((Hp * Wp + 255) / 256), (unsigned)B);
+    hipLaunchKernelGGL(stem_s2d_split_kernel<3>, grid, dim3(256), 0, (hipStream_t)stream, x, C, H, W, pad, dst, plane);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// w [Cout][C][KS][KS] (KS odd, C <= 4) -> split weights of the s2d conv for
+// ubpl_conv2d_forward_psa (Cin = 16, KS' = (KS + 1) / 2 rounded up to even = 4
+// for the 7x7 stem): npieces planes of Cout * KS'^2 * 16 bf16.
+UBPL_API int ubpl_stem_weight_s2d_split(const float* w, int Cout, int C, int KS, int npieces, uint16_t* dst,
+                                        int64_t plane, void* stream) {
+    const int KT = ((KS + 1) / 2 + 1) & ~1;
+    if (C < 1 || C > 4 || !(KS & 1) || npieces != 3 || KT != 4 || (plane % 8) != 0) return (int)hipErrorInvalidValue;
+    const int64_t total = (int64_t)Cout * KT * KT * 16;
+    hipLaunchKernelGGL(stem_weight_s2d_split_kernel<3>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, w, Cout, C, KS, KT, dst, plane);
+    UBPL_LAUNCH_CHECK();
+    return 0;
 }

@@ -59,6 +59,8 @@ SIGNATURES = {
     "ubpl_split_activation": (I, [P, I, I, I, I, P, P, I, I, P, L, P]),
     "ubpl_conv2d_forward_psa_workspace": (L, [I, I, I, I, I, I, I]),
     "ubpl_conv2d_forward_psa": (I, [P, L, I, I, I, I, I, P, L, P, I, I, P, P, P, I, P, P, P, I, P, P]),
+    "ubpl_stem_s2d_split": (I, [P, I, I, I, I, I, I, P, L, P]),
+    "ubpl_stem_weight_s2d_split": (I, [P, I, I, I, I, P, L, P]),
     "ubpl_conv1x1_split_load_preferred": (I, [I, I, I, I]),
     "ubpl_conv1x1_forward_split_load": (I, [P, I, I, I, P, L, P, I, P, P, P, P, P, P, P, I, P, P]),
     "ubpl_maxpool2x2_forward": (I, [P, L, I, I, P, P]),

@@ -41,6 +41,8 @@ _WGRAD1_SPLIT = os.environ.get("UBPL_WGRAD1_SPLIT", "1") != "0"
 # default: the epilogue's x reads sit on the critical path of the big dgrad launches and
 # cost more (-3 % step) than the separate streaming partials pass they replace.
 _BWD_EPI = os.environ.get("UBPL_BWD_EPI", "0") == "1"
+# the 7x7/s2 stem on the split path by space-to-depth (UBPL_STEM_S2D=0: exact-f32 kernel)
+_STEM_S2D = os.environ.get("UBPL_STEM_S2D", "1") != "0"
 # forward BatchNorm statistics from the conv epilogues (UBPL_FWD_EPI=1).  Off by default:
 # epilogue partials + a finalize launch measured 1.3 % slower than the one-launch
 # statistics pass (stats_kernel) on the training step.
@@ -538,7 +540,12 @@ class _Exec:
 
     # ---- layers
     def stem(self, imgs):
-        y0 = self.conv("pre.0.conv", imgs, stride=2)
+        if self.m.conv_pieces == 3 and _STEM_S2D and Kn.stem_s2d_ok(imgs):
+            # 7x7/s2 as a 4x4 stride-1 conv over the space-to-depth image, on the split path
+            ws = Kn.stem_weight_s2d_split(self.m.P("pre.0.conv.weight"))
+            y0 = Kn.conv2d_forward_psa(Kn.stem_s2d_split(imgs, 2), ws, self.m.P("pre.0.conv.bias"))
+        else:
+            y0 = self.conv("pre.0.conv", imgs, stride=2)
         sc, sh = self.bn("pre.0.bn", y0)
         x0 = Kn.bn_apply(y0, sc, sh, relu=1)
         self.save("pre.0", (imgs, y0))

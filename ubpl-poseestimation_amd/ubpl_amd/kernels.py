@@ -481,6 +481,31 @@ def conv2d_forward_psa(xs, ws, bias, res=None, out=None, stat_part=None, bwd=Non
     return y
 
 
+def stem_s2d_ok(x):
+    B, C, H, W = x.shape
+    return C <= 4 and H % 2 == 0 and W % 2 == 0 and (B * (H // 2) * (W // 2)) % 256 == 0
+
+
+def stem_s2d_split(x, pad=2):
+    """7x7/s2 stem input as the 16-channel PSA image of its 4 phase images
+    (space-to-depth; channels c*4 + 2ph + pw, the rest zero), border `pad`."""
+    B, C, H, W = x.shape
+    Ho, Wo = H // 2, W // 2
+    plane = B * (Ho + 2 * pad) * (Wo + 2 * pad) * 16
+    buf = torch.empty(3 * plane, device=x.device, dtype=torch.int16)
+    call("ubpl_stem_s2d_split", _p(x), B, C, H, W, int(pad), 3, _p(buf), int(plane), stream())
+    return SplitAct(buf, plane, B, 16, Ho, Wo, pad, 3)
+
+
+def stem_weight_s2d_split(w):
+    """The stem's 7x7 weights as the split 4x4 weights of its space-to-depth conv."""
+    Cout, C, KS, _ = w.shape
+    plane = Cout * 16 * 16
+    buf = torch.empty(3 * plane, device=w.device, dtype=torch.int16)
+    call("ubpl_stem_weight_s2d_split", _p(w.contiguous()), Cout, C, KS, 3, _p(buf), int(plane), stream())
+    return SplitWeights(buf, plane, 0, (Cout, 16, 16), 3)
+
+
 def conv1x1_split_load_ok(x, ws):
     """The 6xbf16 split-on-load 1x1 kernel takes this shape and fills the chip."""
     B, Cin, H, W = x.shape
