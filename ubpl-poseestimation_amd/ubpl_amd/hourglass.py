@@ -315,6 +315,23 @@ class StackedHourglass(nn.Module):
         o, shp = idx[name]
         return Kn.SplitWeights(buf, plane, o, shp, self.conv_pieces)
 
+    def alt_grad_buffer(self):
+        """Second gradient buffer for a backward pass that runs concurrently with
+        another of the same network (train.py: a student's second view on its
+        idle teacher's stream); merge_alt_grads adds it into flat_grads."""
+        if getattr(self, "_alt_grads", None) is None:
+            self._alt_grads = torch.zeros_like(self.flat_grads)
+            self._alt_pending = []
+        return self._alt_grads
+
+    def merge_alt_grads(self):
+        """flat_grads += the concurrent pass's gradients (on the current stream,
+        after it has joined that pass's stream)."""
+        if getattr(self, "_alt_pending", None):
+            self.flat_grads.add_(self._alt_grads)
+            self._alt_grads.zero_()
+            self._alt_pending = []
+
     def live_params(self):
         return self.flat_params[:self.n_live]
 
@@ -424,6 +441,18 @@ class _HourglassFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dpreds, dfeats):
         model = ctx.model
+        ex = ctx.ex
+        if ex.bwd_stream is not None:
+            # a second view's backward on another (idle) stream, into the
+            # alternate gradient buffer; the caller joins that stream and merges
+            if dfeats is not None and dfeats.numel() == 0:
+                dfeats = None
+            s = ex.bwd_stream
+            s.wait_stream(torch.cuda.current_stream(s.device))
+            with torch.cuda.stream(s):
+                model._backward_impl(ex, dpreds, dfeats)
+            model._alt_pending.append((ex, dpreds, dfeats))   # alive until the join
+            return None, None, None
         # torch optimizers may have reset .grad to None (zero_grad(set_to_none));
         # then the flat buffer is stale and is restarted from zero.
         first = next(iter(model.parameters()))
@@ -445,6 +474,17 @@ class _HourglassFn(torch.autograd.Function):
 class _Exec:
     def __init__(self, model, B, dev, part, train, save):
         self.m, self.B, self.dev, self.part, self.train, self.do_save = model, B, dev, part, train, save
+        # backward on another stream into the alternate gradient buffer (train.py sets
+        # model._bwd_stream around a student's second-view forward)
+        self.bwd_stream = getattr(model, "_bwd_stream", None) if save else None
+        self.gbuf = model.alt_grad_buffer() if self.bwd_stream is not None else model.flat_grads
+        if self.bwd_stream is not None:
+            key = ("alt", B)
+            if key not in model._ws:
+                model._ws[key] = (torch.zeros_like(part), torch.empty(3 * 512, device=dev))
+            self.bpart, self.bcoef = model._ws[key]
+        else:
+            self.bpart, self.bcoef = part, None
         self.saved = {}
         self.saved_split = {}
         self._rp = None     # (tensor, BN partials of it) from its producer, for the next residual's bn1
@@ -593,28 +633,32 @@ class _Exec:
 
     # ---- backward
     def _coef(self):
-        return self.m._ws[("coef", self.B)]
+        return self.bcoef if self.bcoef is not None else self.m._ws[("coef", self.B)]
+
+    def G(self, name):
+        s, n, shp = self.m._offs[name]
+        return self.gbuf[s:s + n].view(shp)
 
     def bn_bwd(self, name, dz, x, relu, add1=None, add2=None, out=None, part=None):
         """part: the backward partials dz's producer wrote (None: a statistics pass)."""
         sc, sh, mu, istd = self.bnc(name)
-        return Kn.bn_backward(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.part, self._coef(),
-                              self.m.G(name + ".weight"), self.m.G(name + ".bias"), add1=add1, add2=add2, out=out,
+        return Kn.bn_backward(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.bpart, self._coef(),
+                              self.G(name + ".weight"), self.G(name + ".bias"), add1=add1, add2=add2, out=out,
                               part=part)
 
     def bn_bwd_split(self, name, dz, x, relu, part=None):
         sc, sh, mu, istd = self.bnc(name)
-        return Kn.bn_backward_split(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.part,
-                                    self._coef(), self.m.G(name + ".weight"), self.m.G(name + ".bias"), 3, 1,
+        return Kn.bn_backward_split(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.bpart,
+                                    self._coef(), self.G(name + ".weight"), self.G(name + ".bias"), 3, 1,
                                     part=part)
 
     def wgrad(self, name, dy, x, KS, stride=1, pro=None):
         ps, ph = (None, None) if pro is None else pro
         if KS == 1 and self.m.conv_pieces == 3 and _WGRAD1_SPLIT and Kn.wgrad1x1_split_load_ok(dy, x):
-            Kn.conv2d_wgrad1x1_split_load(dy, x, self.m.G(name + ".weight"), self.m.G(name + ".bias"), ps, ph,
+            Kn.conv2d_wgrad1x1_split_load(dy, x, self.G(name + ".weight"), self.G(name + ".bias"), ps, ph,
                                           accumulate=True)
             return
-        Kn.conv2d_wgrad(dy, x, KS, stride, self.m.G(name + ".weight"), self.m.G(name + ".bias"), ps, ph,
+        Kn.conv2d_wgrad(dy, x, KS, stride, self.G(name + ".weight"), self.G(name + ".bias"), ps, ph,
                         accumulate=True)
 
     def bwd_epi(self, bn, x):
@@ -665,7 +709,7 @@ class _Exec:
         if split_wgrad:
             # d t2 only as the split operand both conv2 gradients read
             ys = self.bn_bwd_split(p + ".bn3", d, t2, relu=1, part=part)
-            Kn.conv2d_wgrad3_psa(ys, xs, self.m.G(p + ".conv2.conv.weight"), self.m.G(p + ".conv2.conv.bias"))
+            Kn.conv2d_wgrad3_psa(ys, xs, self.G(p + ".conv2.conv.weight"), self.G(p + ".conv2.conv.bias"))
             d = Kn.conv2d_forward_psa(ys, ws, None, bwd=bwd2)         # d relu(bn2(t1))
         elif ws is not None and ws.npieces == 3:
             d = self.bn_bwd(p + ".bn3", d, t2, relu=1, part=part)     # d t2
@@ -700,7 +744,8 @@ class _Exec:
     def backward(self, dpreds, dfeats):
         m = self.m
         S = m.nStack
-        m.relayout_weights(1)
+        if self.bwd_stream is None:     # (the forward laid them out; a concurrent pass only reads them)
+            m.relayout_weights(1)
         dpreds = dpreds.contiguous()
         if dfeats is not None:
             dfeats = dfeats.contiguous()

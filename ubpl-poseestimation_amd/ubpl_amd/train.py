@@ -139,6 +139,10 @@ def _sync_stats(local_sums, counts):
 # ---------------------------------------------------------------------------
 # MT_UBPL
 # ---------------------------------------------------------------------------
+# a student's second-view backward on its teacher's stream (UBPL_SPLIT_BWD=0: one stream per student)
+_SPLIT_BWD = os.environ.get("UBPL_SPLIT_BWD", "1") != "0"
+
+
 class _ModelStreams:
     """One HIP stream per network (students 0..M-1, then their teachers).  The
     networks are independent until the losses, and their small hourglass
@@ -338,11 +342,16 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
     B = imgs[0].shape[0]
     outs, feats, outs_ema = [], [], []
     mstreams = _ModelStreams.make(M, dev)
+    split_bwd = mstreams is not None and _SPLIT_BWD
     for mi in range(M):                                      # :228-243
         oa, fa, ea = [], [], []
         with (mstreams.on(mi) if mstreams else contextlib.nullcontext()):
             for a in range(A):
+                # views >= 1: their backward runs on the teacher's stream (idle by
+                # then) into the alternate gradient buffer, beside view 0's
+                models[mi]._bwd_stream = mstreams.side[M + mi] if split_bwd and a >= 1 else None
                 o, f = models[mi](imgs[a])
+                models[mi]._bwd_stream = None
                 oa.append(o)
                 fa.append(f)
         with (mstreams.on_teacher(mi) if mstreams else contextlib.nullcontext()):
@@ -400,6 +409,8 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
     _backward_all(totals)                                     # :334-336
     if mstreams:
         mstreams.join()
+    for m in models:
+        m.merge_alt_grads()
     D.allreduce_grads(models)
     for o in optims:
         o.step()
