@@ -403,6 +403,17 @@ int splits_for(int B, int C) {
     return s;
 }
 
+// The batch slices a statistics launch actually uses: splits_for's bound, and
+// at least ~8k elements per (channel, slice) block — small planes get one
+// block per channel (at 4x4 / B=32, 2048 blocks of 32 elements each were pure
+// launch and ticket overhead).
+int splits_for(int B, int C, int HW) {
+    int s = splits_for(B, C);
+    const int64_t per_slice = (int64_t)B * HW / 8192;
+    if (s > per_slice) s = per_slice > 1 ? (int)per_slice : 1;
+    return s;
+}
+
 int grid_ew(int64_t n) {
     int64_t g = (n + 255) / 256;
     if (g > 4096) g = 4096;
@@ -551,7 +562,7 @@ UBPL_API int64_t ubpl_bn_part_doubles(int B, int C) { return CNT_DOUBLES + 2 * (
 UBPL_API int ubpl_bn_forward_stats(const float* x, int B, int C, int HW, const float* gamma, const float* beta,
                                    float eps, float momentum, float* rmean, float* rvar, double* part,
                                    float* mean_out, float* invstd_out, float* scale, float* shift, void* stream) {
-    const int splits = splits_for(B, C);
+    const int splits = splits_for(B, C, HW);
     const int bper = (B + splits - 1) / splits;
     const int gs = (B + bper - 1) / bper;
     if (C > MAXBN) return (int)hipErrorInvalidValue;
@@ -632,7 +643,7 @@ int bwd_stats(const float* dz, const float* x, int B, int C, int HW, const float
     const BwdOut o{gamma, invstd, dgamma, dbeta, coef, coef + C, coef + 2 * C};
     if (part == nullptr) {   // one launch: slices + last-arriver combine
         if (C > MAXBN || scratch == nullptr) return (int)hipErrorInvalidValue;
-        const int splits = splits_for(B, C);
+        const int splits = splits_for(B, C, HW);
         const int bper = (B + splits - 1) / splits;
         const int gs = (B + bper - 1) / bper;
         const bool vec = (HW % 4 == 0) && ((((uintptr_t)dz | (uintptr_t)x) & 15) == 0);
