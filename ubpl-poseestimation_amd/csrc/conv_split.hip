@@ -45,6 +45,20 @@ __device__ __forceinline__ void mfma_split(floatx16& acc, const bf16x8 (&a)[NP],
         for (int pa = d; pa >= 0; --pa) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa], b[d - pa], acc, 0, 0, 0);
 }
 
+// the same sum started from zero (one 16-k chunk of the chunked accumulation):
+// the first MFMA takes C = 0 as an inline constant, no zeroed registers
+template <int NP>
+__device__ __forceinline__ floatx16 mfma_split0(const bf16x8 (&a)[NP], const bf16x8 (&b)[NP]) {
+    const floatx16 zero = {};
+    floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[NP - 1], b[0], zero, 0, 0, 0);
+#pragma unroll
+    for (int d = NP - 1; d >= 0; --d)
+#pragma unroll
+        for (int pa = d; pa >= 0; --pa)
+            if (!(d == NP - 1 && pa == NP - 1)) t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa], b[d - pa], t, 0, 0, 0);
+    return t;
+}
+
 // ------------------------------------------------------------------ forward
 // x NCHW f32; wp: NP planes (stride wplane elements) of the grouped tap-major
 // weights [Cout][Ktot] as bf16; Cin % 16 == 0.  Epilogue / split-K slab as
@@ -719,11 +733,7 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 // per-chunk accumulation (see conv_fwd_split_kernel)
-                floatx16 tmp;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) tmp[r] = 0.f;
-                mfma_split<NP>(tmp, af, bfr[j]);
-                acc[i][j] += tmp;
+                acc[i][j] += mfma_split0<NP>(af, bfr[j]);
             }
             // (register budget: one row block's A fragments live at a time)
             __builtin_amdgcn_sched_barrier(0);
