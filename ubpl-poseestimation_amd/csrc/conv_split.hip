@@ -529,11 +529,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
-                    floatx16 tmp;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) tmp[r] = 0.f;
-                    mfma_split<NP>(tmp, af[i], bfr[j]);
-                    acc[i][j] += tmp;
+                    acc[i][j] += mfma_split0<NP>(af[i], bfr[j]);
                 }
         } else if constexpr (NP == 3) {
             // every tile's chunk chain first, the f32 adds after them (behind a
@@ -544,9 +540,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) tmp[i][j][r] = 0.f;
-                    mfma_split<NP>(tmp[i][j], af[i], bfr[j]);
+                    tmp[i][j] = mfma_split0<NP>(af[i], bfr[j]);
                 }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -909,9 +903,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) tmp[i][j][r] = 0.f;
-                mfma_split<NP>(tmp[i][j], af[i], bfr[j]);
+                tmp[i][j] = mfma_split0<NP>(af[i], bfr[j]);
             }
         __builtin_amdgcn_sched_barrier(0);   // chains first, adds after (see conv_psa_kernel)
 #pragma unroll
@@ -1073,9 +1065,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restri
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-#pragma unroll
-                for (int q = 0; q < 16; ++q) tmp[i][j][q] = 0.f;
-                mfma_split<NP>(tmp[i][j], af[i], bfr[j]);
+                tmp[i][j] = mfma_split0<NP>(af[i], bfr[j]);
             }
         __builtin_amdgcn_sched_barrier(0);   // chains first, adds after (see conv_psa_kernel)
 #pragma unroll
