@@ -776,8 +776,12 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
     constexpr int BM = CB, TM = CB / 64, TN = CB / 64, NS = 3;
     constexpr int GR = CB / 16;                            // channel groups per operand tile
     constexpr int PI = GR * 512;                           // piece image: GR groups x 16 px x 32 B
-    constexpr int AB = NP * PI, BB = NP * PI;              // bytes per stage
-    __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
+    constexpr int AB = NP * PI, BB = NP * PI;              // bytes per 16-pixel step
+    // 64-channel tiles carry two 16-pixel steps per stage (one barrier per 12 MFMA
+    // chains instead of 6)
+    constexpr int KS2 = CB == 64 ? 2 : 1;
+    constexpr int SUB = AB + BB;
+    __shared__ __attribute__((aligned(16))) char lds[NS * KS2 * SUB];
     typedef short v4i16 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) v4i16* tr_ptr_t;
 
@@ -812,13 +816,12 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
     const uint32_t b_lane = a_lane;
     const char* dys_m = reinterpret_cast<const char*>(dys + (int64_t)(m0 >> 4) * HWp * 16);
     const char* xs_c = reinterpret_cast<const char*>(xs + (int64_t)(ci0 >> 4) * HWp * 16);
-    auto stage = [&](int buf, int s) {
+    auto stage1 = [&](char* base, int s) {
         const int b = s / (H * wsteps);
         const int rem = s - b * (H * wsteps);
         const int oh = rem / wsteps, ow0 = (rem - oh * wsteps) * 16;
         const int64_t aoff = (int64_t)b * Gco * HWp * 16 + ((int64_t)(oh + 1) * Wp + ow0 + 1) * 16;
         const int64_t boff = (int64_t)b * Gci * HWp * 16 + ((int64_t)(oh + kh) * Wp + ow0 + kw) * 16;
-        char* base = lds + buf * (AB + BB);
         if (!d_issue) return;
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
@@ -829,6 +832,11 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane), (lds_ptr_t)(base + AB + p * PI + wid * 1024),
                                              16, 0, 0);
         }
+    };
+    auto stage = [&](int buf, int s) {   // steps s .. s + KS2 - 1 (those before s_end)
+#pragma unroll
+        for (int u = 0; u < KS2; ++u)
+            if (s + u < s_end) stage1(lds + (buf * KS2 + u) * SUB, s + u);
     };
 
     // transposed-read geometry: 16-lane group g reads channel group (tile base
@@ -861,55 +869,61 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
     const bool bias_wave = tap == bz % 9 && ci0 == 0 && wn == 0;
     float bsum[TM] = {};
 
-    if (nkt > 0) stage(0, s_begin);
-    if (nkt > 1) stage(1, s_begin + 1);
-    for (int t = 0; t < nkt; ++t) {
-        if (t + 1 < nkt) vm_wait<2 * NP>();
+    const int iters = (nkt + KS2 - 1) / KS2;
+    if (iters > 0) stage(0, s_begin);
+    if (iters > 1) stage(1, s_begin + KS2);
+    for (int t = 0; t < iters; ++t) {
+        // counted wait only when the newer stage in flight is a full one
+        if (t + 1 < iters && s_begin + (t + 2) * KS2 <= s_end) vm_wait<2 * NP * KS2>();
         else vm_wait<0>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (t + 2 < nkt) stage((t + 2) % NS, s_begin + t + 2);
-        char* base = lds + (t % NS) * (AB + BB);
-        bf16x8 af[TM][NP], bfr[TN][NP];
+        if (t + 2 < iters) stage((t + 2) % NS, s_begin + (t + 2) * KS2);
 #pragma unroll
-        for (int p = 0; p < NP; ++p) {
+        for (int u = 0; u < KS2; ++u) {
+            if (s_begin + t * KS2 + u >= s_end) break;
+            char* base = lds + ((t % NS) * KS2 + u) * SUB;
+            bf16x8 af[TM][NP], bfr[TN][NP];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * PI + aoffs[i][0]));
-                const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * PI + aoffs[i][1]));
-                const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                af[i][p] = __builtin_bit_cast(bf16x8, v);
+            for (int p = 0; p < NP; ++p) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const v4i16 lo =
+                        __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * PI + aoffs[i][0]));
+                    const v4i16 hi =
+                        __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * PI + aoffs[i][1]));
+                    const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    af[i][p] = __builtin_bit_cast(bf16x8, v);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const v4i16 lo =
+                        __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * PI + boffs[j][0]));
+                    const v4i16 hi =
+                        __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * PI + boffs[j][1]));
+                    const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    bfr[j][p] = __builtin_bit_cast(bf16x8, v);
+                }
             }
+            if (bias_wave) {
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const v4i16 lo =
-                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * PI + boffs[j][0]));
-                const v4i16 hi =
-                    __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * PI + boffs[j][1]));
-                const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                bfr[j][p] = __builtin_bit_cast(bf16x8, v);
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int p = 0; p < NP; ++p)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) bsum[i] += (float)af[i][p][e];
             }
-        }
-        if (bias_wave) {
+            floatx16 tmp[TM][TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int p = 0; p < NP; ++p)
+                for (int j = 0; j < TN; ++j) tmp[i][j] = mfma_split0<NP>(af[i], bfr[j]);
+            __builtin_amdgcn_sched_barrier(0);   // chains first, adds after (see conv_psa_kernel)
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) bsum[i] += (float)af[i][p][e];
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] += tmp[i][j];
         }
-        floatx16 tmp[TM][TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                tmp[i][j] = mfma_split0<NP>(af[i], bfr[j]);
-            }
-        __builtin_amdgcn_sched_barrier(0);   // chains first, adds after (see conv_psa_kernel)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] += tmp[i][j];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 
@@ -933,6 +947,163 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
             const float v = bsum[i] + __shfl_xor(bsum[i], 32, 64);
             if (h == 0) sl[(int64_t)(m0 + wm + 32 * i + li) * Nt + Ntot] = v;
         }
+    }
+}
+
+// 64-channel 3x3 weight gradient (wgrad3_psa_kernel's operands and slab): an
+// n-tile is one kernel ROW — the 3 taps (kh, 0..2) x 64 input channels — so a
+// wave's tile is 32 output channels x 96 (3 taps x 32 channels): 18 MFMA
+// chains per barrier instead of 6 with 64 x 64 one-tap tiles.  Stage image: A
+// [piece][4 groups][16 px][32 B], then B per tap kw [piece][4 groups][16 px][32 B]
+// (the three taps' shifted pixel windows DMA'd separately); wave 0 moves A,
+// wave 1 + kw moves tap kw of B (6 DMA instructions each per stage).
+template <int NP>
+__global__ void __launch_bounds__(NT, 2) wgrad3_psa64_kernel(const uint16_t* __restrict__ dys, int64_t dplane,
+                                                            const uint16_t* __restrict__ xs, int64_t xplane, int B,
+                                                            int Cin, int Cout, int H, int W, int steps_per_split,
+                                                            float* __restrict__ slab) {
+    constexpr int TN = 3, NS = 3;
+    constexpr int PI = 4 * 512;               // piece image: 4 groups x 16 px x 32 B
+    constexpr int OB = NP * PI;               // one operand image (A, or one tap of B)
+    constexpr int SB = 4 * OB;                // stage: A + 3 taps of B
+    __shared__ __attribute__((aligned(16))) char lds[NS * SB];
+    typedef short v4i16 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4i16* tr_ptr_t;
+
+    const int Hp = H + 2, Wp = W + 2;
+    const int Gci = Cin >> 4, Gco = Cout >> 4;
+    const int Ntot = 9 * Cin, Nt = Ntot + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = (wid >> 1) * 32, wn = (wid & 1) * 96;
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                              gridDim.x * gridDim.y * gridDim.z);
+    const int bx = lam % gridDim.x, by = (lam / gridDim.x) % gridDim.y, bz = lam / (gridDim.x * gridDim.y);
+    const int m0 = by * 64;
+    const int nci = Cin / 64;
+    const int kh = bx / nci, ci0 = (bx - kh * nci) * 64;
+    const int wsteps = W >> 4;
+    const int total_steps = B * H * wsteps;
+    const int s_begin = bz * steps_per_split;
+    const int s_end = min(total_steps, s_begin + steps_per_split);
+    const int nkt = max(0, s_end - s_begin);
+
+    // DMA: group pair gp (2 groups, one per half-wave), the swizzled pixel row
+    const int64_t HWp = (int64_t)Hp * Wp;
+    const int rphys = (lane & 31) >> 1;
+    uint32_t lane_off[2];
+#pragma unroll
+    for (int gp = 0; gp < 2; ++gp) {
+        const int gl = 2 * gp + (lane >> 5);
+        const int rlog = rphys ^ (4 * (gl & 1));
+        lane_off[gp] = (uint32_t)(((gl * HWp + rlog) * 16 + 8 * (lane & 1)) * 2);
+    }
+    const char* dys_m = reinterpret_cast<const char*>(dys + (int64_t)(m0 >> 4) * HWp * 16);
+    const char* xs_c = reinterpret_cast<const char*>(xs + (int64_t)(ci0 >> 4) * HWp * 16);
+    const int kw_w = wid - 1;   // the B tap this wave moves (waves 1..3)
+    auto stage = [&](int buf, int s) {
+        const int b = s / (H * wsteps);
+        const int rem = s - b * (H * wsteps);
+        const int oh = rem / wsteps, ow0 = (rem - oh * wsteps) * 16;
+        char* base = lds + buf * SB;
+        const char* src;
+        int64_t plane;
+        if (wid == 0) {
+            src = dys_m + 2 * ((int64_t)b * Gco * HWp * 16 + ((int64_t)(oh + 1) * Wp + ow0 + 1) * 16);
+            plane = dplane;
+        } else {
+            src = xs_c + 2 * ((int64_t)b * Gci * HWp * 16 + ((int64_t)(oh + kh) * Wp + ow0 + kw_w) * 16);
+            plane = xplane;
+            base += OB * (1 + kw_w);
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int gp = 0; gp < 2; ++gp)
+                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + 2 * p * plane + lane_off[gp]),
+                                                 (lds_ptr_t)(base + p * PI + gp * 1024), 16, 0, 0);
+    };
+
+    // transposed-read geometry (as wgrad3_psa_kernel)
+    const int g16 = lane >> 4, i16 = lane & 15;
+    const int qrow = i16 >> 2, pcol = i16 & 3;
+    auto tr_off = [&](int grp, int t) {
+        const int row = (8 * (g16 >> 1) + 4 * t + qrow) ^ (4 * (grp & 1));
+        return grp * 512 + row * 32 + 8 * pcol;
+    };
+    int aoffs[2], boffs[TN][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) aoffs[t] = tr_off(wm / 16 + (g16 & 1), t);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int nb = wn / 32 + j;   // 32-column block: tap nb/2, channels 32*(nb&1) ..
+#pragma unroll
+        for (int t = 0; t < 2; ++t) boffs[j][t] = OB * (1 + (nb >> 1)) + tr_off(2 * (nb & 1) + (g16 & 1), t);
+    }
+
+    floatx16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const bool bias_wave = kh == bz % 3 && ci0 == 0 && wn == 0;
+    float bsum = 0.f;
+
+    if (nkt > 0) stage(0, s_begin);
+    if (nkt > 1) stage(1, s_begin + 1);
+    for (int t = 0; t < nkt; ++t) {
+        if (t + 1 < nkt) vm_wait<2 * NP>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + 2 < nkt) stage((t + 2) % NS, s_begin + t + 2);
+        const char* base = lds + (t % NS) * SB;
+        bf16x8 af[NP], bfr[TN][NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            {
+                const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * PI + aoffs[0]));
+                const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * PI + aoffs[1]));
+                const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                af[p] = __builtin_bit_cast(bf16x8, v);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * PI + boffs[j][0]));
+                const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * PI + boffs[j][1]));
+                const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                bfr[j][p] = __builtin_bit_cast(bf16x8, v);
+            }
+        }
+        if (bias_wave) {
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bsum += (float)af[p][e];
+        }
+        floatx16 tmp[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) tmp[j] = mfma_split0<NP>(af, bfr[j]);
+        __builtin_amdgcn_sched_barrier(0);   // chains first, adds after (see conv_psa_kernel)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[j] += tmp[j];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    float* sl = slab + (int64_t)bz * Cout * Nt;
+    const int li = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int nb = wn / 32 + j;
+        const int n = (kh * 3 + (nb >> 1)) * Cin + ci0 + 32 * (nb & 1) + li;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+            sl[(int64_t)m * Nt + n] = acc[j][r];
+        }
+    }
+    if (bias_wave) {
+        const float v = bsum + __shfl_xor(bsum, 32, 64);
+        if (h == 0) sl[(int64_t)(m0 + wm + li) * Nt + Ntot] = v;
     }
 }
 
@@ -1516,7 +1687,8 @@ int wgrad3_cb(int Cin, int Cout) { return (Cin % 128 == 0 && Cout % 128 == 0) ? 
 
 int wgrad3_splits(int B, int Cin, int Cout, int H, int W) {
     const int cb = wgrad3_cb(Cin, Cout);
-    const int tiles = 9 * (Cin / cb) * (Cout / cb);
+    // 128: one tap x 128 channels per n-tile; 64: one kernel row (3 taps) x 64 channels
+    const int tiles = cb == 128 ? 9 * (Cin / cb) * (Cout / cb) : 3 * (Cin / 64) * (Cout / 64);
     const int steps = B * H * (W / 16);
     int s = 512 / tiles;                               // one round of 2 workgroups per CU, not one over
     if (s < 1) s = 1;
@@ -1546,13 +1718,15 @@ UBPL_API int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t
     const int steps = B * H * (W / 16);
     const int per = (steps + splits - 1) / splits;
     const int cb = wgrad3_cb(Cin, Cout);
-    dim3 grid((unsigned)(9 * (Cin / cb)), (unsigned)(Cout / cb), (unsigned)splits);
-    if (cb == 128)
+    if (cb == 128) {
+        dim3 grid((unsigned)(9 * (Cin / cb)), (unsigned)(Cout / cb), (unsigned)splits);
         hipLaunchKernelGGL((wgrad3_psa_kernel<3, 128>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout,
                            H, W, per, slab);
-    else
-        hipLaunchKernelGGL((wgrad3_psa_kernel<3, 64>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout,
-                           H, W, per, slab);
+    } else {
+        dim3 grid((unsigned)(3 * (Cin / 64)), (unsigned)(Cout / 64), (unsigned)splits);
+        hipLaunchKernelGGL((wgrad3_psa64_kernel<3>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout, H,
+                           W, per, slab);
+    }
     UBPL_LAUNCH_CHECK();
     return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 9, db != nullptr, dw, db, accumulate, stream);
 }
