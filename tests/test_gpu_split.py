@@ -226,6 +226,7 @@ SOL_CASES = [
     (3, 64, 32, 64, True, True),
     (5, 256, 8, 256, False, True),
     (3, 128, 6, 128, True, False),
+    (16, 128, 64, 256, True, True),       # 256-row 8-wave tiles (one pixel tile per CU)
 ]
 
 
