@@ -284,6 +284,12 @@ def test_pool_upsample_vs_torch():
     dout = torch.randn(2, 8, 16, 16, generator=gen)
     out.backward(dout)
     _close(Kn.upsample2x_add(up.to(DEV), low.detach().to(DEV)), out, rtol=0, atol=0)
+    ud = up.to(DEV)                                   # in place (out aliases up), float4 path
+    Kn.upsample2x_add(ud, low.detach().to(DEV), out=ud)
+    _close(ud, out, rtol=0, atol=0)
+    u6, l3 = torch.randn(2, 3, 6, 6, generator=gen), torch.randn(2, 3, 3, 3, generator=gen)   # W % 4 != 0
+    _close(Kn.upsample2x_add(u6.to(DEV), l3.to(DEV)), u6 + F.interpolate(l3, scale_factor=2, mode="nearest"),
+           rtol=0, atol=0)
     dl = torch.zeros(2, 8, 8, 8, device=DEV)
     Kn.upsample2x_add_backward(dout.to(DEV), dl, accumulate=False)
     _close(dl, low.grad, rtol=1e-6, atol=1e-6)
