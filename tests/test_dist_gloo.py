@@ -66,7 +66,9 @@ def _worker(rank, world, port, q):
         fake = types.SimpleNamespace(flat_params=torch.full((5,), float(rank + 1)),
                                      flat_stats=torch.full((3,), float(rank + 7)))
         D.broadcast_params([fake])
-        q.put((rank, g, float(glob), fake.flat_params.clone(), fake.flat_stats.clone(), D.world(), D.rank()))
+        # plain lists: a tensor would travel as a shared-memory fd that dies with this process
+        q.put((rank, g.tolist(), float(glob), fake.flat_params.tolist(), fake.flat_stats.tolist(),
+               D.world(), D.rank()))
     finally:
         dist.destroy_process_group()
 
@@ -89,9 +91,9 @@ def test_dp_global_normalisers_match_single_process():
     loss.backward()
     for rank, g, glob, fp, fs, world, rk in res:
         assert world == 2 and rk == rank
-        torch.testing.assert_close(g, w.grad, rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(torch.tensor(g), w.grad, rtol=1e-5, atol=1e-7)
         assert abs(glob - loss.item()) <= 1e-5 * abs(loss.item())
-        assert torch.equal(fp, torch.full((5,), 1.0)) and torch.equal(fs, torch.full((3,), 7.0))
+        assert fp == [1.0] * 5 and fs == [7.0] * 3
 
 
 def test_single_process_helpers_are_identity():
