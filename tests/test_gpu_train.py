@@ -150,8 +150,10 @@ def test_step_graph_replay_matches_eager(monkeypatch):
 
     p_e, s_e, r_e = run(False)
     p_g, s_g, r_g = run(True)
+    diag = {"params": [float((a - b).abs().max()) for a, b in zip(p_e, p_g)],
+            "stats": [float((a - b).abs().max()) for a, b in zip(s_e, s_g)]}
     for a, b in zip(p_e, p_g):
-        assert torch.equal(a, b)
+        assert torch.equal(a, b), diag
     for a, b in zip(s_e, s_g):
-        assert torch.equal(a, b)
+        assert torch.equal(a, b), diag
     assert _flat(r_e, []) == _flat(r_g, [])
