@@ -112,3 +112,32 @@ def test_tools_weights_cpu():
         assert np.array_equal(ProjectTools.getSampleWeight([isl], a)[0].numpy(), g[case + "/w"])
         assert np.array_equal(ProjectTools.getSampleWeight_nega([isl], a)[0].numpy(), g[case + "/w_nega"])
         assert np.array_equal(ProjectTools.getSampleWeight_mt_cons(isl, a).numpy(), g[case + "/w_mt_cons"])
+
+
+def test_checkpoint_schema_and_selection_cpu(tmp_path):
+    """ubpl_amd.checkpoint on plain torch modules / AdamW (host logic only):
+    projects/MT_UBPL.py:88-103 selection rule and key schema, comm.py file names."""
+    import types
+    import torch
+    from ubpl_amd import checkpoint as CK
+    args = types.SimpleNamespace(best_acc=[0.3, 0.3, 0.3], best_epoch=[1, 1, 1])
+    assert CK.select_best([[0.2, 0.3], [0.9, 0.31], [0.5, 0.1]], args, 7) == [False, True, False]
+    assert args.best_acc == [0.3, 0.31, 0.3] and args.best_epoch == [1, 7, 1]
+    torch.manual_seed(0)
+    ms = [torch.nn.Linear(3, 2) for _ in range(2)]
+    es = [torch.nn.Linear(3, 2) for _ in range(2)]
+    os_ = [torch.optim.AdamW(m.parameters(), lr=1e-3) for m in ms]
+    for m, o in zip(ms, os_):
+        m(torch.ones(1, 3)).sum().backward()
+        o.step()
+    ck = CK.checkpoint_state(ms, es, os_, args, 7)
+    assert list(ck) == ["current_epoch", "best_acc", "best_epoch", "model1_state", "model1_ema_state",
+                        "optim1_state", "model2_state", "model2_ema_state", "optim2_state"]
+    path = CK.save_checkpoint(ck, False, str(tmp_path / "ckpts"))
+    assert path.endswith("ckpts/checkpoint.pth.tar") and not (tmp_path / "ckpts" / "checkpoint_best.pth.tar").exists()
+    ms2 = [torch.nn.Linear(3, 2) for _ in range(2)]
+    es2 = [torch.nn.Linear(3, 2) for _ in range(2)]
+    os2 = [torch.optim.AdamW(m.parameters(), lr=1e-3) for m in ms2]
+    assert CK.load_checkpoint(path, ms2, es2, os2) == (7, [0.3, 0.31, 0.3], [1, 7, 1])
+    assert torch.equal(ms2[1].weight, ms[1].weight) and torch.equal(es2[0].bias, es[0].bias)
+    assert float(os2[0].state_dict()["state"][0]["step"]) == 1.0

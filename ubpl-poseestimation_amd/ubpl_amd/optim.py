@@ -43,12 +43,76 @@ class FlatAdamW:
                            g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self._step_t,
                            self._coef)
 
+    # -- checkpoints: torch.optim.AdamW's state_dict layout -----------------
+    # projects/MT_UBPL.py:97-103 stores optims[b].state_dict() in the
+    # checkpoint next to the models' state_dicts (utils/base/comm.py:92-103
+    # torch.save).  The state is laid out exactly as torch.optim.AdamW lays it
+    # out over model.parameters() (reference order, 454 tensors for HG2): one
+    # entry per parameter that has been stepped (the live ones; the dead
+    # skip_layer parameters never get a gradient, so torch keeps no state for
+    # them either), 'step' a CPU float tensor, group keys from torch itself.
+    # Checkpoints interchange both ways with the reference's optimizers.
+    def _group_template(self):
+        g = self.param_groups[0]
+        probe = torch.optim.AdamW([torch.zeros(1, requires_grad=True)], lr=g["lr"], betas=g["betas"], eps=g["eps"],
+                                  weight_decay=g["weight_decay"])
+        grp = dict(probe.state_dict()["param_groups"][0])
+        grp.update({k: v for k, v in g.items()})
+        return grp
+
+    def _live_slices(self):
+        m = self.model
+        for i, (name, _) in enumerate(m.named_parameters()):
+            s, n, shp = m._offs[name]
+            yield i, s, n, shp, s < m.n_live
+
     def state_dict(self):
-        return {"state": {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq},
-                "param_groups": [dict(self.param_groups[0])]}
+        names = list(self.model.named_parameters())
+        grp = self._group_template()
+        grp["params"] = list(range(len(names)))
+        state = {}
+        step = self.step_count
+        if step > 0:
+            for i, s, n, shp, live in self._live_slices():
+                if live:
+                    state[i] = {"step": torch.tensor(float(step)),
+                                "exp_avg": self.exp_avg[s:s + n].view(shp).clone(),
+                                "exp_avg_sq": self.exp_avg_sq[s:s + n].view(shp).clone()}
+        return {"state": state, "param_groups": [grp]}
 
     def load_state_dict(self, sd):
-        self._step_t.fill_(int(sd["state"]["step"]))
-        self.exp_avg.copy_(sd["state"]["exp_avg"])
-        self.exp_avg_sq.copy_(sd["state"]["exp_avg_sq"])
-        self.param_groups[0].update(sd["param_groups"][0])
+        """Accepts torch.optim.AdamW's layout over model.parameters() (a
+        reference checkpoint's optim<b>_state, or this class's state_dict)."""
+        groups = sd["param_groups"]
+        if len(groups) != 1:
+            raise ValueError("FlatAdamW holds one parameter group, the state has %d" % len(groups))
+        nparams = sum(1 for _ in self.model.parameters())
+        if len(groups[0]["params"]) != nparams:
+            raise ValueError("loaded state dict has a group of %d parameters, the model has %d"
+                             % (len(groups[0]["params"]), nparams))
+        pos = {pid: i for i, pid in enumerate(groups[0]["params"])}
+        st = {pos[k]: v for k, v in sd["state"].items()}
+        steps = set()
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+        for i, s, n, shp, live in self._live_slices():
+            e = st.get(i)
+            if e is None:
+                continue
+            if not live:
+                raise ValueError("state for parameter %d, which never receives a gradient here" % i)
+            if tuple(e["exp_avg"].shape) != tuple(shp):
+                raise ValueError("state shape %s for parameter %d of shape %s" % (tuple(e["exp_avg"].shape), i,
+                                                                                  tuple(shp)))
+            self.exp_avg[s:s + n].copy_(e["exp_avg"].reshape(-1))
+            self.exp_avg_sq[s:s + n].copy_(e["exp_avg_sq"].reshape(-1))
+            steps.add(int(float(e["step"])))
+        if len(steps) > 1:
+            raise ValueError("per-parameter step counts differ (%s): one flat step count cannot hold them"
+                             % sorted(steps))
+        self._step_t.fill_(steps.pop() if steps else 0)
+        g = groups[0]
+        if g.get("amsgrad") or g.get("maximize"):
+            raise ValueError("FlatAdamW runs plain AdamW (amsgrad / maximize unsupported)")
+        self.lr, self.betas, self.eps, self.weight_decay = g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]
+        self.param_groups[0].update(lr=g["lr"], betas=tuple(g["betas"]), eps=g["eps"], weight_decay=g["weight_decay"])
