@@ -83,6 +83,13 @@ int ubpl_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, dou
  * call), so a captured HIP graph of the training step replays it; coef: 4 floats. */
 int ubpl_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
                         double beta2, double eps, double weight_decay, int64_t* step, float* coef, void* stream);
+/* ubpl_adamw_step_dev on p[0, nlive) fused with ubpl_ema_update(ema, p, n) in
+ * one pass (the optimizer step of projects/MT_UBPL.py:338-340 followed by
+ * update_ema_variables, utils/parameters.py:4-8); bit-identical to the two
+ * calls.  nlive, n multiples of 4; buffers 16-B aligned. */
+int ubpl_adamw_ema_step_dev(float* p, const float* g, float* m, float* v, int64_t nlive, double lr, double beta1,
+                            double beta2, double eps, double weight_decay, int64_t* step, float* coef, float* ema,
+                            int64_t n, double alpha, void* stream);
 int ubpl_scale_(float* x, int64_t n, float s, void* stream);
 
 /* ---------------------------------------------------------------- H2-H4 --

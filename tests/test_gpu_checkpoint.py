@@ -115,3 +115,34 @@ def test_resume_both_directions(tmp_path):
     assert torch.equal(o3.exp_avg, o2.exp_avg) and o3.step_count == o2.step_count
     assert torch.equal(e3.state_dict()["hgs.0.0.up1.bn1.running_mean"],
                        model.state_dict()["hgs.0.0.up1.bn1.running_mean"])
+
+
+def test_fused_adamw_ema_bit_identical_to_separate():
+    """FlatAdamW.step_and_ema (one pass) == step() followed by
+    update_ema_variables (utils/parameters.py:4-8), bit for bit, incl. the
+    never-trained tail the EMA still blends."""
+    import types
+    from ubpl_amd.hourglass import StackedHourglass
+    from ubpl_amd.optim import FlatAdamW
+    from ubpl_amd.parameters import ema_alpha, update_ema_variables
+    torch.manual_seed(0)
+    sa, ta = StackedHourglass(16, 1, "AvgPool"), StackedHourglass(16, 1, "AvgPool")
+    sb, tb = StackedHourglass(16, 1, "AvgPool"), StackedHourglass(16, 1, "AvgPool")
+    sb.load_state_dict(sa.state_dict())
+    tb.load_state_dict(ta.state_dict())
+    oa, ob = FlatAdamW(sa, lr=1e-3, weight_decay=0.01), FlatAdamW(sb, lr=1e-3, weight_decay=0.01)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for epo in (1, 3):
+        args = types.SimpleNamespace(epo=epo, ema_decay=0.999)
+        gr = torch.randn(sa.n_total, device="cuda", generator=g)
+        sa.flat_grads.copy_(gr)
+        sb.flat_grads.copy_(gr)
+        oa.step()
+        update_ema_variables(sa, ta, args)
+        ob.step_and_ema(tb, ema_alpha(epo, 0.999))
+    torch.cuda.synchronize()
+    assert torch.equal(sa.flat_params, sb.flat_params)
+    assert torch.equal(ta.flat_params, tb.flat_params)
+    assert torch.equal(oa.exp_avg, ob.exp_avg) and torch.equal(oa.exp_avg_sq, ob.exp_avg_sq)
+    assert oa.step_count == ob.step_count == 2
+    assert not torch.equal(ta.flat_params[sa.n_live:], sa.flat_params[sa.n_live:])   # tail blended, not copied

@@ -55,6 +55,11 @@ __device__ __forceinline__ bool last_arriver(unsigned* cnt, unsigned n) {
 // parallel (one round trip, not one per slice: a serial read chain here was
 // ~10 % of the training step) and sum them in a fixed tree order
 // (deterministic).  Returns true in lane 0 of that block, with the totals.
+// Doubles between two channels' slice partials: 2 per slice, rounded up to
+// 256 B, so no two channels' partials share a cache line (their publishers
+// and last arrivers may sit on different XCDs, each with its own L2).
+__host__ __device__ __forceinline__ int64_t chan_stride(int nsp) { return ((int64_t)2 * nsp + 31) / 32 * 32; }
+
 __device__ __forceinline__ bool combine_slices(double* pc, int sp, int nsp, unsigned* cnt, double d1, double d2,
                                                double& t1, double& t2) {
     if (threadIdx.x >= 64) return false;
@@ -118,7 +123,7 @@ __global__ void __launch_bounds__(256) stats_kernel(const float* __restrict__ x,
     const double d1 = ubpl::block_sum((double)s1, red);
     const double d2 = ubpl::block_sum((double)s2, red);
     double t1, t2;
-    if (!combine_slices(part + (int64_t)c * gridDim.y * 2, sp, gridDim.y, cnt + c, d1, d2, t1, t2)) return;
+    if (!combine_slices(part + (int64_t)c * chan_stride(gridDim.y), sp, gridDim.y, cnt + c, d1, d2, t1, t2)) return;
     const int64_t N = (int64_t)B * HW;
     const double m1 = t1 / (double)N;
     double var = t2 / (double)N - m1 * m1;
@@ -232,7 +237,7 @@ __global__ void __launch_bounds__(256) bwd_stats_kernel(const float* __restrict_
     const double d1 = ubpl::block_sum((double)s1, red);
     const double d2 = ubpl::block_sum((double)s2, red);
     double t1, t2;
-    if (!combine_slices(part + (int64_t)c * gridDim.y * 2, sp, gridDim.y, cnt + c, d1, d2, t1, t2)) return;
+    if (!combine_slices(part + (int64_t)c * chan_stride(gridDim.y), sp, gridDim.y, cnt + c, d1, d2, t1, t2)) return;
     const double N = (double)((int64_t)B * HW);
     const double is = o.invstd[c], g = o.gamma[c];
     if (o.dgamma) o.dgamma[c] += (float)(t2 * is);
@@ -425,8 +430,8 @@ int grid_ew(int64_t n) {
 
 // Scratch: part must hold ubpl_bn_part_doubles(B, C) doubles, ZEROED before
 // first use: MAXBN arrival counters at its head (a fixed place, whatever C a
-// call has; every call leaves them at zero again), then 2 * C * splits
-// partial sums.
+// call has; every call leaves them at zero again), then per channel the
+// 2 * splits partial sums, channels chan_stride(splits) doubles apart.
 constexpr int MAXBN = 512;
 constexpr int CNT_DOUBLES = MAXBN / 2;
 // ---- statistics from 64-pixel partials (conv-epilogue fused: common.h
@@ -555,7 +560,7 @@ UBPL_API int ubpl_bn_stats_from_partials(const float* part, int C, int64_t N, co
     UBPL_LAUNCH_CHECK();
     return 0;
 }
-UBPL_API int64_t ubpl_bn_part_doubles(int B, int C) { return CNT_DOUBLES + 2 * (int64_t)C * splits_for(B, C); }
+UBPL_API int64_t ubpl_bn_part_doubles(int B, int C) { return CNT_DOUBLES + (int64_t)C * chan_stride(splits_for(B, C)); }
 
 // Train-mode statistics of x [B,C,H,W] -> mean, invstd, (scale, shift) and the
 // running-stat update (rmean/rvar nullable: track_running_stats off).

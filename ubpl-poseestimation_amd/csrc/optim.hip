@@ -107,6 +107,47 @@ __global__ void __launch_bounds__(256) adamw_dev_kernel(float* __restrict__ p, c
         adamw_one(p[i], g[i], m[i], v[i], decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
 }
 
+// AdamW on the student's live prefix and the Mean-Teacher EMA of the whole
+// buffer in one pass: element i < nlive takes the AdamW step
+// and the teacher reads the updated value from registers; nlive <= i < n (the
+// never-trained parameters) only the EMA.  Same per-element arithmetic as
+// adamw_dev_kernel followed by ema_kernel, so results are bit-identical to the
+// two launches, with one read of p (and one launch) fewer.
+__global__ void __launch_bounds__(256) adamw_ema_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                           float* __restrict__ m, float* __restrict__ v,
+                                                           int64_t nlive4, const float* __restrict__ coef,
+                                                           float omb1, float b2, float omb2, float eps,
+                                                           float* __restrict__ ema, int64_t n4, float alpha,
+                                                           float oma) {
+    const float decay = coef[0], bc2_sqrt = coef[1], neg_step = coef[2];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    float4* p4 = reinterpret_cast<float4*>(p);
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    float4* m4 = reinterpret_cast<float4*>(m);
+    float4* v4 = reinterpret_cast<float4*>(v);
+    float4* e4 = reinterpret_cast<float4*>(ema);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 pp = p4[i];
+        float4 e = e4[i];
+        if (i < nlive4) {
+            float4 mm = m4[i], vv = v4[i];
+            const float4 gg = g4[i];
+            adamw_one(pp.x, gg.x, mm.x, vv.x, decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
+            adamw_one(pp.y, gg.y, mm.y, vv.y, decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
+            adamw_one(pp.z, gg.z, mm.z, vv.z, decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
+            adamw_one(pp.w, gg.w, mm.w, vv.w, decay, omb1, b2, omb2, bc2_sqrt, eps, neg_step);
+            p4[i] = pp;
+            m4[i] = mm;
+            v4[i] = vv;
+        }
+        e.x = fmaf(pp.x, oma, e.x * alpha);
+        e.y = fmaf(pp.y, oma, e.y * alpha);
+        e.z = fmaf(pp.z, oma, e.z * alpha);
+        e.w = fmaf(pp.w, oma, e.w * alpha);
+        e4[i] = e;
+    }
+}
+
 __global__ void __launch_bounds__(256) scale_kernel(float* __restrict__ x, int64_t n, float s) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= s;
@@ -164,6 +205,26 @@ UBPL_API int ubpl_adamw_step_dev(float* p, const float* g, float* m, float* v, i
     hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, coef,
                        (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
                        vec4_count(n, p, g, m, v));
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+// ubpl_adamw_step_dev on p[0, nlive) fused with ubpl_ema_update(ema, p, n):
+// flat buffers, 16-B aligned, nlive and n multiples of 4 (the flat layouts pad
+// every segment to 4 floats).  alpha = min(1 - 1/(epo+1), ema_decay)
+// (utils/parameters.py:4-8).
+UBPL_API int ubpl_adamw_ema_step_dev(float* p, const float* g, float* m, float* v, int64_t nlive, double lr,
+                                     double beta1, double beta2, double eps, double weight_decay, int64_t* step,
+                                     float* coef, float* ema, int64_t n, double alpha, void* stream) {
+    if (n <= 0 || nlive < 0 || nlive > n || (nlive & 3) || (n & 3)) return (int)hipErrorInvalidValue;
+    if (vec4_count(n, p, ema) == 0 || (nlive > 0 && vec4_count(nlive, p, g, m, v) == 0))
+        return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(adamw_prep_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step, lr, beta1, beta2,
+                       weight_decay, coef);
+    UBPL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(adamw_ema_dev_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v,
+                       nlive >> 2, coef, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, ema,
+                       n >> 2, (float)alpha, (float)(1.0 - alpha));
     UBPL_LAUNCH_CHECK();
     return 0;
 }

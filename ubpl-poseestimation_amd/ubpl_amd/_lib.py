@@ -27,6 +27,7 @@ SIGNATURES = {
     "ubpl_ema_update": (I, [P, P, L, D, P]),
     "ubpl_adamw_step": (I, [P, P, P, P, L, D, D, D, D, D, L, P]),
     "ubpl_adamw_step_dev": (I, [P, P, P, P, L, D, D, D, D, D, P, P, P]),
+    "ubpl_adamw_ema_step_dev": (I, [P, P, P, P, L, D, D, D, D, D, P, P, P, L, D, P]),
     "ubpl_scale_": (I, [P, L, F, P]),
     "ubpl_bn_splits": (I, [I, I]),
     "ubpl_bn_part_doubles": (L, [I, I]),

@@ -192,6 +192,14 @@ def adamw_step_dev_(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step_t, coe
     call("ubpl_adamw_step_dev", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
          float(eps), float(weight_decay), _p(step_t), _p(coef), stream())
 
+def adamw_ema_step_dev_(p, g, m, v, nlive, lr, beta1, beta2, eps, weight_decay, step_t, coef, ema, alpha):
+    """adamw_step_dev_ on p[:nlive] and ema_update_(ema, p, alpha) over all of p, one pass."""
+    if ema.numel() != p.numel() or nlive > p.numel():
+        raise ValueError("adamw_ema_step_dev_: ema / p / nlive sizes disagree")
+    call("ubpl_adamw_ema_step_dev", _p(p), _p(g), _p(m), _p(v), int(nlive), float(lr), float(beta1), float(beta2),
+         float(eps), float(weight_decay), _p(step_t), _p(coef), _p(ema), p.numel(), float(alpha), stream())
+
+
 def scale_(x, s):
     _chk(x, "x")
     call("ubpl_scale_", _p(x), x.numel(), float(s), stream())

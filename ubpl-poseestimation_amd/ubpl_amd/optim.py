@@ -43,6 +43,16 @@ class FlatAdamW:
                            g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], self._step_t,
                            self._coef)
 
+    def step_and_ema(self, ema_model, alpha):
+        """step() then update_ema_variables(model, ema_model) with this alpha, in
+        one pass over the flat buffers (bit-identical to the two calls)."""
+        if not isinstance(ema_model, StackedHourglass) or ema_model.n_total != self.model.n_total:
+            raise ValueError("step_and_ema: the teacher must be a StackedHourglass of the same architecture")
+        g = self.param_groups[0]
+        Kn.adamw_ema_step_dev_(self.model.flat_params, self.model.flat_grads, self.exp_avg, self.exp_avg_sq,
+                               self.model.n_live, g["lr"], g["betas"][0], g["betas"][1], g["eps"],
+                               g["weight_decay"], self._step_t, self._coef, ema_model.flat_params, alpha)
+
     # -- checkpoints: torch.optim.AdamW's state_dict layout -----------------
     # projects/MT_UBPL.py:97-103 stores optims[b].state_dict() in the
     # checkpoint next to the models' state_dicts (utils/base/comm.py:92-103

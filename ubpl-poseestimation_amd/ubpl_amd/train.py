@@ -185,6 +185,28 @@ class _ModelStreams:
                 t.record_stream(self.main)
 
 
+# AdamW + the EMA teacher update in one pass per model (FlatAdamW.step_and_ema);
+# UBPL_FUSED_EMA=0 runs the optimizer step and update_ema_variables separately.
+_FUSED_EMA = os.environ.get("UBPL_FUSED_EMA", "1") != "0"
+
+
+def _step_and_ema(models, models_ema, optims, args):
+    """optims[i].step() for every student, then update_ema_variables(student,
+    teacher) (projects/MT_UBPL.py:338-344, DualPose_UBPL.py:281-287); the
+    teacher of model i depends only on student i's updated weights, so the
+    per-model fused pass gives the same bits."""
+    from .parameters import ema_alpha
+    if _FUSED_EMA and all(hasattr(o, "step_and_ema") and o.model is m for o, m in zip(optims, models)):
+        a = ema_alpha(args.epo, args.ema_decay)
+        for o, e in zip(optims, models_ema):
+            o.step_and_ema(e, a)
+        return
+    for o in optims:
+        o.step()
+    for mi, m in enumerate(models):
+        update_ema_variables(m, models_ema[mi], args)
+
+
 def _backward_all(totals):
     """The reference runs total_i.backward(retain_graph=True) once per student
     (projects/MT_UBPL.py:334-336): the shared FDL term makes every call reach
@@ -412,10 +434,7 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
     for m in models:
         m.merge_alt_grads()
     D.allreduce_grads(models)
-    for o in optims:
-        o.step()
-    for mi, m in enumerate(models):
-        update_ema_variables(m, models_ema[mi], args)
+    _step_and_ema(models, models_ema, optims, args)
     # ---- records: one device->host copy
     g_rec = []
     for mi in range(M):
@@ -539,10 +558,7 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
             totals.append(pec + mtc + epc + fdc)
         _backward_all(totals)                                     # DualPose_UBPL.py:277-279
         D.allreduce_grads(models)
-        for o in optims:
-            o.step()
-        for mi, m in enumerate(models):
-            update_ema_variables(m, models_ema[mi], args)
+        _step_and_ema(models, models_ema, optims, args)
         g_rec = []
         for mi in range(M):
             g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[6 * mi + 1]),
