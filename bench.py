@@ -235,8 +235,10 @@ def main():
     warm = [batches[i % 2] for i in range(a.warmup)]
     timed = [batches[i % 2] for i in range(a.steps)]
 
-    # the step is captured as a HIP graph on the last warm-up step (train.py
-    # _StepGraph), so the timed steps are replays
+    # default step: eager launches, one HIP stream per network (the captured
+    # step graph is off with per-network streams: open race, DESIGN.md §6;
+    # UBPL_STEP_GRAPH=1 forces it — then it is captured on the last warm-up
+    # step and the timed steps are replays)
     T._StepGraph.WARM = max(1, a.warmup - 1)
     T.train_mt_ubpl(warm, models, emas, optims, args, verbose=False)
     torch.cuda.synchronize()

@@ -207,6 +207,26 @@ def _step_and_ema(models, models_ema, optims, args):
         update_ema_variables(m, models_ema[mi], args)
 
 
+class _OnMain(torch.autograd.Function):
+    """Identity applied on the main stream to a network output produced on a
+    side stream.  Autograd sums the several loss gradients of a tensor on the
+    stream of the node that consumes them; without this node that is the
+    network's stream, reading summands the loss backward allocated on main,
+    which the caching allocator hands back to main once autograd drops them —
+    while the side stream may still be reading them (a race that only shows
+    when main is not the legacy null stream, i.e. in the captured step and
+    its warm-up).  With it, the sum happens on main and the network's backward
+    receives one tensor that lives until its node has run."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
 def _backward_all(totals):
     """The reference runs total_i.backward(retain_graph=True) once per student
     (projects/MT_UBPL.py:334-336): the shared FDL term makes every call reach
@@ -272,8 +292,14 @@ class _StepGraph:
 
     def __init__(self, core, models, models_ema, optims, args):
         self.core, self.models, self.emas, self.optims, self.args = core, models, models_ema, optims, args
-        self.enabled = (os.environ.get("UBPL_STEP_GRAPH", "1") != "0" and not D.is_dist()
-                        and all(hasattr(o, "_step_t") for o in optims))
+        # default: captured only when the networks share one stream.  With
+        # per-network streams the captured step (and its eager warm-up on a
+        # non-null stream) diverges from the eager step now and then (DESIGN.md
+        # §6, open race); UBPL_STEP_GRAPH=1 forces capture, =0 disables it.
+        env = os.environ.get("UBPL_STEP_GRAPH")
+        streams = len(models) >= 2 and os.environ.get("UBPL_MODEL_STREAMS", "1") != "0"
+        want = (env == "1") if env is not None else not streams
+        self.enabled = want and not D.is_dist() and all(hasattr(o, "_step_t") for o in optims)
         self.n_eager = 0
         self.graph = None
         self.key = None
@@ -385,6 +411,9 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
         outs_ema.append(ea)
     if mstreams:
         mstreams.join([t for grp in (outs, feats, outs_ema) for ts in grp for t in ts])
+        # the losses' gradients for each student output are summed on main
+        outs = [[_OnMain.apply(t) for t in ts] for ts in outs]
+        feats = [[None if t is None else _OnMain.apply(t) for t in ts] for ts in feats]
     K = outs[0][0].shape[2]
     # ---- loss sums / counts on device
     sums, cnts = [], []
