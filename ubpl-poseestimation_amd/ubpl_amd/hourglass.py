@@ -198,6 +198,7 @@ class StackedHourglass(nn.Module):
                 mod.register_buffer("num_batches_tracked", self._nbt[self._bn_index[b]])
         self._grad_views_attached = False
         self._ws = {}
+        self._grad_keep = []          # upstream gradients alive until their stream is joined
         # re-laid-out conv weights, rebuilt by one launch per forward (tap-major
         # [Cout][T][Cin] for KS > 1) and per backward (dgrad [Cin][T][Cout]):
         # tables per conv precision, see set_conv_precision / _build_weight_tables
@@ -331,6 +332,7 @@ class StackedHourglass(nn.Module):
             self.flat_grads.add_(self._alt_grads)
             self._alt_grads.zero_()
             self._alt_pending = []
+        self._grad_keep = []
 
     def live_params(self):
         return self.flat_params[:self.n_live]
@@ -389,6 +391,8 @@ class StackedHourglass(nn.Module):
         B = imgs.shape[0]
         dev = imgs.device
         part = self._scratch(B, 64)
+        if save:
+            self._grad_keep = []     # the last step's upstream gradients (its streams joined since)
         ex = _Exec(self, B, dev, part, train=self.training, save=save)
         self.relayout_weights(0)
         self.relayout_weights(1)       # k-major 1x1 weights for conv1x1_forward_kmajor
@@ -462,6 +466,13 @@ class _HourglassFn(torch.autograd.Function):
             model.attach_grad_views()
         if dfeats is not None and dfeats.numel() == 0:
             dfeats = None
+        # the upstream gradients come from the loss backward on the main stream
+        # and are read here on this network's stream; kept alive until the
+        # caller has joined that stream (merge_alt_grads), or the caching
+        # allocator hands their blocks back to main while these kernels still
+        # read them (a race that shows once nothing paces the launches: the
+        # captured step)
+        model._grad_keep.append((dpreds, dfeats))
         # the saved activations stay with ctx: the reference runs backward(retain_graph=True)
         # once per student and the shared FDL term reaches both networks twice
         model._backward_impl(ctx.ex, dpreds, dfeats)
@@ -744,8 +755,10 @@ class _Exec:
     def backward(self, dpreds, dfeats):
         m = self.m
         S = m.nStack
-        if self.bwd_stream is None:     # (the forward laid them out; a concurrent pass only reads them)
-            m.relayout_weights(1)
+        # the data-gradient weights (mode 1) were laid out by the forward
+        # (_forward_impl) and the weights are unchanged since: no re-layout
+        # here, which would rewrite them while a concurrent pass of the same
+        # network (a second view on the teacher's stream) reads them
         dpreds = dpreds.contiguous()
         if dfeats is not None:
             dfeats = dfeats.contiguous()
