@@ -12,24 +12,27 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import determinism as D  # noqa: E402
 
 
+STEPS = int(os.environ.get("PROBE_STEPS", "4"))
+
+
 def one(mode):
     if mode == "eager-side":
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            r = D.run(False, True, 4)
+            r = D.run(False, True, STEPS)
         torch.cuda.synchronize()
         return r
     if mode == "graph-nosplit":
-        return D.run(True, False, 4)
-    return D.run(True, True, 4)
+        return D.run(True, False, STEPS)
+    return D.run(True, True, STEPS)
 
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["graph"]
-    e = D.run(False, True, 4)
-    e0 = D.run(False, False, 4)
+    e = D.run(False, True, STEPS)
+    e0 = D.run(False, False, STEPS)
     for mode in modes:
         ref = e0 if mode == "graph-nosplit" else e
         bad = 0
@@ -38,8 +41,7 @@ def main():
             ds = {k: max(float((x - y).abs().max()) for x, y in zip(ref[k], g[k])) for k in ref}
             bad += max(ds.values()) != 0.0
             print("%s rep %d %s" % (mode, i, " ".join("%s=%.3g" % kv for kv in ds.items())), flush=True)
-        print("%s (UBPL_CAPTURE_RECORD=%s): %d of %d differ" % (mode, os.environ.get("UBPL_CAPTURE_RECORD"), bad,
-                                                                reps), flush=True)
+        print("%s (%d steps): %d of %d differ" % (mode, STEPS, bad, reps), flush=True)
 
 
 if __name__ == "__main__":
