@@ -68,79 +68,107 @@ def make_batches(n, B, K, dev, seed):
     return out
 
 
-class ConvTimer:
-    """HIP events around every launch of the dominant kernel — the Residual conv2
-    forward (3x3, fused BN+ReLU operand) — on the current stream, which the
-    kernel is launched on.  Precision 'f32': kernels.conv2d_forward
-    (conv_fwd_kernel, exact-f32 MFMA); '6xbf16': kernels.conv2d_forward_psa
-    (conv_psa_kernel, split-bf16 MFMA; its BN+ReLU+split pass is a separate
-    kernel and not part of the timed launch)."""
+ROOF_SHAPE = (128, 128, 3, 64, 64)   # Cin, Cout, KS, H, W of the roofline kernel's launches
 
-    def __init__(self, Kn):
-        self.Kn = Kn
-        self.orig = Kn.conv2d_forward
-        self.orig_psa = Kn.conv2d_forward_psa
-        self.events = []
-        self.flops = 0
-        self.active = False
-        self.kind = None
+
+class PsaLaunches:
+    """Records, during one eager step, the C-ABI argument tuple of every
+    ubpl_conv2d_forward_psa call whose shape is the roofline kernel's — the
+    3x3 128->128 convs on the 64x64 planes (Residual conv2 forward and its
+    data gradient), which run as ONE instantiation, conv_psa_kernel<128, 3, 3,
+    256, 2> (rocprofv3 names it so), with no split-K slab — and keeps every
+    tensor those pointers reference alive, so the launches can be replayed."""
+
+    def __init__(self, Kn, lib):
+        self.Kn, self.lib = Kn, lib
+        self.calls, self.keep = [], []
 
     def __enter__(self):
-        orig, orig_psa = self.orig, self.orig_psa
+        orig_call, orig_psa = self.lib.call, self.Kn.conv2d_forward_psa
+        self._orig = (orig_call, orig_psa)
+        rec = self
 
-        def wrapped_psa(xs, ws, bias, res=None, out=None, stat_part=None, bwd=None):
-            if not self.active or ws.shape[1] != 9 or bias is None:
-                return orig_psa(xs, ws, bias, res, out, stat_part, bwd)
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
+        def call(name, *args):
+            if name == "ubpl_conv2d_forward_psa" and rec._want:
+                rec.calls.append(args)
+            return orig_call(name, *args)
+
+        def psa(xs, ws, bias, res=None, out=None, stat_part=None, bwd=None):
+            Cout, T, _ = ws.shape
+            rec._want = (xs.C, Cout, int(round(T ** 0.5)), xs.H, xs.W) == ROOF_SHAPE
             y = orig_psa(xs, ws, bias, res, out, stat_part, bwd)
-            e.record()
-            self.events.append((s, e))
-            self.kind = "psa"
-            self.flops += 2 * xs.B * ws.shape[0] * xs.C * 9 * xs.H * xs.W
+            if rec._want:
+                rec.keep.append((xs, ws, bias, res, y, stat_part, bwd))
+            rec._want = False
             return y
-        self.Kn.conv2d_forward_psa = wrapped_psa
-
-        def wrapped(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out=None, w_tap=None):
-            if not self.active or w is None or w.shape[-1] != 3 or pscale is None:
-                return orig(x, w, bias, stride, pscale, pshift, res, out, w_tap)
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            y = orig(x, w, bias, stride, pscale, pshift, res, out, w_tap)
-            e.record()
-            self.events.append((s, e))
-            self.kind = "f32"
-            B, Cin = x.shape[:2]
-            Cout = w.shape[0]
-            self.flops += 2 * B * Cout * Cin * 9 * y.shape[-1] * y.shape[-2]
-            return y
-        self.Kn.conv2d_forward = wrapped
+        self._want = False
+        self.lib.call = call
+        self.Kn.call = call
+        self.Kn.conv2d_forward_psa = psa
         return self
 
     def __exit__(self, *a):
-        self.Kn.conv2d_forward = self.orig
-        self.Kn.conv2d_forward_psa = self.orig_psa
+        self.lib.call = self._orig[0]
+        self.Kn.call = self._orig[0]
+        self.Kn.conv2d_forward_psa = self._orig[1]
 
-    def result(self):
+    def time(self, reps=10):
+        """Replays the recorded launches back to back (reps times, queue filled
+        behind a spin kernel so no host gap enters the window) between two HIP
+        events on the stream they were launched on; returns the average
+        duration of one launch in ms."""
+        fn = self.lib.lib().ubpl_conv2d_forward_psa
+        calls = [c for c in self.calls if c[14] is None]        # slab pointer: none (no split-K)
+        if not calls:
+            return None, 0
         torch.cuda.synchronize()
-        n = len(self.events)
-        if n == 0:
-            return None
-        ms = sum(s.elapsed_time(e) for s, e in self.events)
-        avg_ms = ms / n
-        flops_per_launch = self.flops / n
-        achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
-        if self.kind == "psa":
-            peak, kernel = SPLIT6_PEAK_TFLOPS, ("conv_psa_kernel<3x3, 6xbf16 split-f32 MFMA> (Residual conv2); "
-                                                "achieved/peak in f32-equivalent FLOP/s, peak = bf16 dense / 6")
-        else:
-            peak, kernel = F32_MFMA_PEAK_TFLOPS, "conv_fwd_kernel<3x3,f32 MFMA> (Residual conv2)"
-        pmc = pmc_traffic(self.kind)
-        return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": (pmc or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc,
-                "kernel": kernel, "launches": n,
-                "avg_launch_us": round(avg_ms * 1e3, 2), "flops_per_launch": int(flops_per_launch)}
+        for c in calls:                                         # warm
+            self.lib.check(fn(*c), "ubpl_conv2d_forward_psa")
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(20_000_000)
+        s.record()
+        for _ in range(reps):
+            for c in calls:
+                fn(*c)
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / (reps * len(calls)), len(calls)
+
+
+def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step):
+    """The dominant kernel: conv_psa_kernel<128,3,3,256,2> (3x3 conv on the
+    6xbf16 split path at the 64x64 planes, forward + data gradient; the
+    largest single entry of the rocprofv3 kernel summary, profiles/r02_*).
+    achieved = algorithmic f32-equivalent FLOP per launch (2*B*Cout*Cin*9*H*W)
+    / its average standalone launch duration (HIP events around replayed
+    launches, see PsaLaunches.time), vs 2.5 PF bf16 dense / 6 piece products."""
+    os.environ["UBPL_MODEL_STREAMS"] = "0"
+    try:
+        with PsaLaunches(Kn, lib) as rec, T._StepGraph.eager():
+            T.train_mt_ubpl([batch], models, emas, optims, args, verbose=False)
+        torch.cuda.synchronize()
+        avg_ms, n = rec.time()
+    finally:
+        del os.environ["UBPL_MODEL_STREAMS"]
+    if avg_ms is None:
+        return None
+    Cin, Cout, KS, H, W = ROOF_SHAPE
+    B = args.batch
+    flops = 2 * B * Cout * Cin * KS * KS * H * W
+    achieved = flops / (avg_ms * 1e-3) / 1e12
+    per_step_ms = n * avg_ms
+    assert per_step_ms <= ms_per_step, (per_step_ms, ms_per_step)
+    pmc = pmc_traffic("psa")
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(SPLIT6_PEAK_TFLOPS, 2),
+            "unit": "TFLOP/s", "frac": round(achieved / SPLIT6_PEAK_TFLOPS, 4),
+            "traffic": (pmc or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc,
+            "kernel": "conv_psa_kernel<128, 3, 3, 256, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
+                      "6xbf16 split-f32 MFMA; f32-equivalent FLOP/s, peak = bf16 dense / 6)",
+            "flops_per_launch": flops, "launches_per_step": n, "avg_launch_us": round(avg_ms * 1e3, 2),
+            "kernel_ms_per_step": round(per_step_ms, 3),
+            "timing": "HIP events around back-to-back replays of the step's launches of this kernel "
+                      "(standalone; inputs resident), after the timed region"}
 
 
 def pmc_traffic(kind):
@@ -157,13 +185,18 @@ def pmc_traffic(kind):
             "write_bytes_per_launch": int(d["write_bytes_per_launch"]), "source": d.get("source")}
 
 
-def cpu_baseline(steps=2, B=4):
-    """The oracle's CPU restatement of the same MT_UBPL step (oracle/step.py),
-    timed on this host's cores on a bounded sample."""
+def cpu_baseline(steps=1, B=32):
+    """The oracle's CPU restatement of the same MT_UBPL step (oracle/step.py,
+    pinned to the reference's own train() outputs by tests/test_oracle_golden.py),
+    timed on this host on a bounded sample: ONE step of the headline workload
+    (B=32, 2 stacks, 256x256, K=16) after one untimed B=4 step.  Threads: the
+    CPU share of a GPU box (16; os.cpu_count() reports the whole machine).
+    Calibrated against the reference's train() itself in the build container:
+    profiles/r02_cpu_calibration.json."""
     from oracle import hourglass as OH
     from oracle import render as OR
     from oracle import step as OS
-    threads = min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("UBPL_CPU_THREADS", min(16, os.cpu_count() or 1)))
     torch.set_num_threads(threads)
     torch.manual_seed(1388)
     models, emas, optims = [], [], []
@@ -174,22 +207,27 @@ def cpu_baseline(steps=2, B=4):
         emas.append(e)
         optims.append(torch.optim.AdamW(models[-1].parameters(), lr=2.5e-4, weight_decay=0))
     args = make_args(B)
-    args.nStack = 2
-    batches = []
-    for (imgs, _, meta) in make_batches(steps + 1, B, 16, "cpu", 77):
-        hms, gates = [], []
-        for k in meta["kps"]:
-            h, kk = OR.render_batch(k.numpy(), (256, 256), 256, 64)
-            hms.append([torch.from_numpy(h)])
-            gates.append([torch.from_numpy(kk[:, :, 2].copy())])
-        batches.append((imgs, hms, {"kpsWeights": gates, "islabeled": meta["islabeled"]}))
-    OS.train_mt_ubpl(batches[:1], models, emas, optims, args)      # warm-up
+
+    def host_batches(n, b, seed):
+        out = []
+        for (imgs, _, meta) in make_batches(n, b, 16, "cpu", seed):
+            hms, gates = [], []
+            for k in meta["kps"]:
+                h, kk = OR.render_batch(k.numpy(), (256, 256), 256, 64)
+                hms.append([torch.from_numpy(h)])
+                gates.append([torch.from_numpy(kk[:, :, 2].copy())])
+            out.append((imgs, hms, {"kpsWeights": gates, "islabeled": meta["islabeled"]}))
+        return out
+    OS.train_mt_ubpl(host_batches(1, 4, 76), models, emas, optims, args)      # warm-up
+    batches = host_batches(steps, B, 77)
     t = time.time()
-    OS.train_mt_ubpl(batches[1:], models, emas, optims, args)
+    OS.train_mt_ubpl(batches, models, emas, optims, args)
     dt = time.time() - t
     return {"value": round(steps * B / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": "oracle/step.py MT_UBPL step (same math as projects/MT_UBPL.py:157), 2-stack, "
-                      "B=%d (half labeled), 256x256, K=16, %d timed steps, torch CPU fp32" % (B, steps)}
+            "sample": "oracle/step.py MT_UBPL step (same math as projects/MT_UBPL.py:157-352), 2-stack, "
+                      "B=%d (half labeled), 256x256, K=16, %d timed step(s) = %.1f s, torch CPU fp32; "
+                      "calibration vs the reference's train(): profiles/r02_cpu_calibration.json"
+                      % (B, steps, dt)}
 
 
 def main():
@@ -252,21 +290,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    # roofline kernel: host events cannot be recorded inside a captured graph,
-    # so its launches are timed on one more (eager, untimed) step of the same
-    # workload right after the timed region, with the networks run one after
-    # another so each launch has the GPU to itself (in the timed steps up to
-    # four networks' kernels overlap, which stretches every launch)
-    os.environ["UBPL_MODEL_STREAMS"] = "0"
-    with ConvTimer(Kn) as ct, T._StepGraph.eager():
-        ct.active = True
-        T.train_mt_ubpl(timed[:1], models, emas, optims, args, verbose=False)
-        ct.active = False
-    del os.environ["UBPL_MODEL_STREAMS"]
-    roof = ct.result()
-    if roof is not None:
-        roof["timing"] = ("HIP events around each launch (its stream), one eager step after the timed region, "
-                          "networks serialised")
+    # roofline kernel: its launches from one more (eager, untimed) step, replayed
+    # back to back between HIP events (standalone duration; see roofline())
+    args.batch = B
+    roof = roofline(Kn, _lib, T, models, emas, optims, args, timed[0], dt / a.steps * 1e3)
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

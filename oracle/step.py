@@ -38,8 +38,9 @@ def _fdc(features_a, features_b, sw, args):
     return L.joint_feature_dist(v1, v2)
 
 
-def train_mt_ubpl(loader, models, emas, optims, args):
-    """projects/MT_UBPL.py:157-352."""
+def train_mt_ubpl(loader, models, emas, optims, args, on_grads=None):
+    """projects/MT_UBPL.py:157-352.  on_grads(models) is called with the
+    students' final gradients, just before the optimizer steps."""
     M = len(models)
     pec_c = [AvgCounter() for _ in range(M)]
     mtc_c = [AvgCounter() for _ in range(M)]
@@ -86,16 +87,21 @@ def train_mt_ubpl(loader, models, emas, optims, args):
             pec.append(args.poseWeight * _norm(s, n))
             pec_c[mi].update(pec[-1].item(), n)
         n_ps, n_sel = 0, 0
-        for mi in range(M):                                        # :271-291
-            s, n = 0., 0
-            for a in range(A):
-                tg = torch.stack([outs_ema[j][a] for j in range(M)]).detach()
-                ls, ln, ns, _, _, _ = L.joint_pseudo3(outs[mi][a], tg, nega, args.nStack, args.pseudoScoreThr)
-                s, n = s + ls, n + ln
-                n_ps, n_sel = n_ps + ln, n_sel + ns
-            epc.append(args.ensemblePseudoWeight * _norm(s, n))
-            epc_c[mi].update(epc[-1].item(), n)
-        counts.append((n_sel, n_ps))
+        if getattr(args, "useEnsemblePseudo", True):
+            for mi in range(M):                                    # :271-291
+                s, n = 0., 0
+                for a in range(A):
+                    tg = torch.stack([outs_ema[j][a] for j in range(M)]).detach()
+                    ls, ln, ns, _, _, _ = L.joint_pseudo3(outs[mi][a], tg, nega, args.nStack, args.pseudoScoreThr)
+                    s, n = s + ls, n + ln
+                    n_ps, n_sel = n_ps + ln, n_sel + ns
+                epc.append(args.ensemblePseudoWeight * _norm(s, n))
+                epc_c[mi].update(epc[-1].item(), n)
+            counts.append((n_sel, n_ps))
+        else:                                                      # :292-293
+            epc = [0.] * M
+            for c in epc_c:
+                c.update(0., imgs[0].shape[0])
         if args.FDLWeight <= 0:                                     # :298-330
             fdc = 0.
             fdc_c.update(0., imgs[0].shape[0])
@@ -108,6 +114,8 @@ def train_mt_ubpl(loader, models, emas, optims, args):
             fdc_c.update(fdc.item(), n)
         for mi in range(M):                                        # :334-336 (fdc in both totals)
             (pec[mi] + mtc[mi] + epc[mi] + fdc).backward(retain_graph=True)
+        if on_grads is not None:
+            on_grads(models)
         for o in optims:
             o.step()
         _ema_all(models, emas, args)                               # :338
@@ -115,7 +123,7 @@ def train_mt_ubpl(loader, models, emas, optims, args):
     return rec, counts
 
 
-def train_dualpose_ubpl(loader, models, emas, optims, args):
+def train_dualpose_ubpl(loader, models, emas, optims, args, on_grads=None):
     """projects/DualPose_UBPL.py:156-295."""
     M = len(models)
     pec_c = [AvgCounter() for _ in range(M)]
@@ -156,22 +164,29 @@ def train_dualpose_ubpl(loader, models, emas, optims, args):
             pec.append(args.poseWeight * _norm(s, n))
             pec_c[mi].update(pec[-1].item(), n)
         e_ps, e_sel = 0, 0
-        for mi in range(M):                                        # :226-236
-            s, n, nsel, _, _, _ = L.joint_pseudo3(outs[mi], outs_ema.detach(), nega, args.nStack,
-                                                  args.pseudoScoreThr)
-            e_ps, e_sel = e_ps + n, e_sel + nsel
-            epc.append(args.ensemblePseudoWeight * _norm(s, n))
-            epc_c[mi].update(epc[-1].item(), n)
-        counts.append((e_sel, e_ps))
+        if getattr(args, "useEnsemblePseudo", True):
+            for mi in range(M):                                    # :226-236
+                s, n, nsel, _, _, _ = L.joint_pseudo3(outs[mi], outs_ema.detach(), nega, args.nStack,
+                                                      args.pseudoScoreThr)
+                e_ps, e_sel = e_ps + n, e_sel + nsel
+                epc.append(args.ensemblePseudoWeight * _norm(s, n))
+                epc_c[mi].update(epc[-1].item(), n)
+            counts.append((e_sel, e_ps))
+        else:                                                      # :243-245 (outs.shape[2] = nStack)
+            epc = [0.] * M
+            for c in epc_c:
+                c.update(0., args.nStack)
         if args.FDLWeight <= 0:
             fdc = 0.
-            fdc_c.update(0., stu_img.shape[0])
+            fdc_c.update(0., args.nStack)                         # :249 outs.shape[2] = nStack
         else:
             cs, cn = _fdc(feats[0], feats[1], sw, args)             # :246-270
             fdc = args.FDLWeight * _norm(cs, cn)
             fdc_c.update(fdc.item(), cn)
         for mi in range(M):
             (pec[mi] + mtc[mi] + epc[mi] + fdc).backward(retain_graph=True)
+        if on_grads is not None:
+            on_grads(models)
         for o in optims:
             o.step()
         _ema_all(models, emas, args)
@@ -179,7 +194,7 @@ def train_dualpose_ubpl(loader, models, emas, optims, args):
     return rec, counts
 
 
-def train_mt(loader, model, ema, optim, args):
+def train_mt(loader, model, ema, optim, args, on_grads=None):
     """projects/MT.py:161-268 (one student + EMA teacher)."""
     pec_c, mtc_c = AvgCounter(), AvgCounter()
     model.train()
@@ -208,12 +223,14 @@ def train_mt(loader, model, ema, optim, args):
         pec = args.poseWeight * _norm(s, n)
         pec_c.update(pec.item(), n)
         (pec + mtc).backward()
+        if on_grads is not None:
+            on_grads([model])
         optim.step()
         _ema_all([model], [ema], args)
     return (pec_c.avg, mtc_c.avg), []
 
 
-def train_supervised(loader, model, optim, args):
+def train_supervised(loader, model, optim, args, on_grads=None):
     """projects/supervised.py:135-175."""
     pec_c = AvgCounter()
     model.train()
@@ -224,5 +241,7 @@ def train_supervised(loader, model, optim, args):
         pec = args.poseWeight * _norm(s, n)
         pec_c.update(pec.item(), n)
         pec.backward()
+        if on_grads is not None:
+            on_grads([model])
         optim.step()
     return pec_c.avg, []

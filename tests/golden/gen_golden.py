@@ -294,10 +294,17 @@ def _import_project(name):
 def gen_steps(R):
     out = {}
     for cname, cfg in seeds.step_cases().items():
+        print("  step case", cname, flush=True)
         proj = _import_project(cfg["project"])
         models, emas, optims = seeds.step_models(R["SH"], cfg)
         before = [[p.detach().clone() for p in m.parameters()] for m in models + emas]
         loader, args = seeds.step_batch(cfg, R["P"].kps_heatmap)
+        # each student's gradients as the reference's optimizer sees them (step pre-hook)
+        grads = {}
+        for mi, (m, o) in enumerate(zip(models, optims)):
+            def hook(opt, a, kw, m=m, mi=mi):
+                grads[mi] = seeds.grad_record([(n, p.grad) for n, p in m.named_parameters()])
+            o.register_step_pre_hook(hook)
         buf = io.StringIO()
         with contextlib.redirect_stdout(buf):
             if cfg["project"] in ("MT_UBPL", "DualPose_UBPL"):
@@ -321,6 +328,8 @@ def gen_steps(R):
             out[cname + "/model%d/psum" % mi] = np.array(psum)
             _, bst = _buf_stats(m)
             out[cname + "/model%d/buf" % mi] = bst
+            if mi in grads:
+                out[cname + "/model%d/grad_stats" % mi], out[cname + "/model%d/grad_samp" % mi] = grads[mi]
     np.savez_compressed(os.path.join(HERE, "steps.npz"), **out)
 
 

@@ -195,6 +195,8 @@ def hg_cases():
         "hg2": dict(K=16, S=2, mode="AvgPool", seed=1388, B=2, res=256, sub=4, iseed=501),
         "hg1k17": dict(K=17, S=1, mode="default", seed=7, B=1, res=128, sub=2, iseed=502),
         "hg4max": dict(K=17, S=4, mode="MaxPool", seed=9, B=1, res=128, sub=2, iseed=503),
+        # BASELINE.json configs[4]: 8 stacks at 384x384 input / 96x96 heatmaps
+        "hg8_384": dict(K=16, S=8, mode="AvgPool", seed=11, B=2, res=384, sub=4, iseed=504),
     }
 
 
@@ -228,6 +230,16 @@ def step_cases():
                    mode="AvgPool", brNum=1, A=2, seed=604),
         "sup": dict(base, project="supervised", S=1, K=16, B=4, nlab=4, epo=0, consWeight=0.0,
                     thr=0.95, mode="default", brNum=1, A=1, seed=605),
+        # useEnsemblePseudo False + FDL_type 'distance' (projects/MT_UBPL.py:271-330 else branches)
+        "mt_ubpl_noep": dict(base, project="MT_UBPL", S=2, K=16, B=4, nlab=2, epo=1, consWeight=3.0,
+                             thr=0.15, mode="AvgPool", brNum=2, A=2, seed=606, useEnsemblePseudo=False,
+                             FDL_type="distance"),
+        # BASELINE.json configs[3]: DualPose_UBPL, dual 4-stack hourglasses, K=17
+        "dualpose_hg4": dict(base, project="DualPose_UBPL", S=4, K=17, B=4, nlab=2, epo=3, consWeight=5.0,
+                             thr=0.15, mode="AvgPool", brNum=2, A=1, seed=607, pseudoWeight=0.5),
+        # the headline config (BASELINE.json configs[1..2]): MT_UBPL, 2 stacks, B=32 (16 labeled)
+        "mt_ubpl_b32": dict(base, project="MT_UBPL", S=2, K=16, B=32, nlab=16, epo=1, consWeight=10.0,
+                            thr=0.15, mode="AvgPool", brNum=2, A=2, seed=608),
     }
 
 
@@ -298,12 +310,35 @@ def step_batch(cfg, render):
                 "islabeled": [isl]}
         batch = (imgs, [[hms[a]] for a in range(A)], meta)
     args = types.SimpleNamespace(
-        device="cpu", debug=False, br_augNum=1, br_gtNum=1, nStack=cfg["S"], useEnsemblePseudo=True,
+        device="cpu", debug=False, br_augNum=1, br_gtNum=1, nStack=cfg["S"],
+        useEnsemblePseudo=cfg.get("useEnsemblePseudo", True),
         pseudoScoreThr=cfg["thr"], ensemblePseudoWeight=cfg["ensemblePseudoWeight"],
         consWeight=cfg["consWeight"], poseWeight=cfg["poseWeight"], FDLWeight=cfg["FDLWeight"],
         FDL_label=cfg["FDL_label"], FDL_type=cfg["FDL_type"], epo=cfg["epo"], ema_decay=cfg["ema_decay"],
         pseudoWeight=cfg["pseudoWeight"], lr=cfg["lr"], feature_mode=cfg["mode"])
     return [batch], args
+
+
+def grad_sample_idx(n, k=8):
+    """Fixed element indices sampled from a parameter's flattened gradient."""
+    return np.unique(np.linspace(0, n - 1, min(n, k)).astype(np.int64))
+
+
+def grad_record(named_grads, k=8):
+    """Per-parameter gradient record stored in steps.npz: [sum, sum of squares,
+    sum of |g|] and k sampled elements (NaN padded)."""
+    st, samp = [], []
+    for _, g in named_grads:
+        if g is None:
+            st.append([0.0, 0.0, 0.0])
+            samp.append([np.nan] * k)
+            continue
+        v = g.detach().double().reshape(-1).cpu()
+        st.append([v.sum().item(), (v * v).sum().item(), v.abs().sum().item()])
+        idx = grad_sample_idx(v.numel(), k)
+        row = v[torch.from_numpy(idx)].numpy().tolist()
+        samp.append(row + [np.nan] * (k - len(row)))
+    return np.array(st), np.array(samp)
 
 
 def bn_cancelled(name):

@@ -96,6 +96,101 @@ def test_dp_global_normalisers_match_single_process():
         assert fp == [1.0] * 5 and fs == [7.0] * 3
 
 
+def _fdl_data():
+    g = torch.Generator().manual_seed(3)
+    B, C, S, Cf, R = 8, 5, 2, 6, 4
+    x = torch.randn(B, C, R, R, generator=g)
+    isl = torch.tensor([1, 0, 1, 1, 0, 0, 1, 0], dtype=torch.bool)   # rank 1 (odd rows) has 1 labeled row
+    wa = torch.randn(S * Cf, C, 1, 1, generator=g)
+    wb = torch.randn(S * Cf, C, 1, 1, generator=g)
+    return x, isl, wa, wb, (S, Cf)
+
+
+def _feats(w, x, S, Cf):
+    y = torch.nn.functional.conv2d(x, w)
+    return y.reshape(x.shape[0], S, Cf, y.shape[-2], y.shape[-1])
+
+
+def _fdl_local_views(wa, wb, x, isl, S, Cf, kind):
+    """The per-view (kind, value, n_loc) triples train._fdl_view produces,
+    computed with the oracle's restatement on this rank's selected rows."""
+    from oracle import losses as OL
+    fa, fb = _feats(wa, x, S, Cf), _feats(wb, x, S, Cf)
+    views = []
+    for a in range(2):                                   # two views: the second one shifted
+        f1, f2 = (fa, fb) if a == 0 else (fa * 0.5 + 0.1, fb - 0.2)
+        rows = isl
+        n_rows = int(rows.sum())
+        if kind == "cov":
+            if n_rows:
+                v, n = OL.features_cov(f1[rows], f2[rows])
+            else:
+                v, n = torch.zeros(()) * wa.sum(), 0
+            views.append(("cov", v, torch.tensor([float(n)])))
+        else:
+            v, n = OL.joint_feature_dist(f1[rows], f2[rows]) if n_rows else (torch.zeros(()) * wa.sum(), 0)
+            views.append(("dist", v, torch.tensor([float(n)])))
+    return views
+
+
+def _fdl_worker(rank, world, port, q, kind):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ubpl_amd import dist as D
+        from ubpl_amd.train import _fdl_record, _fdl_record_sums, _fdl_total, _sync_stats
+        x, isl, wa0, wb0, (S, Cf) = _fdl_data()
+        sl = slice(rank, None, world)
+        wa, wb = wa0.clone().requires_grad_(True), wb0.clone().requires_grad_(True)
+        views = _fdl_local_views(wa, wb, x[sl], isl[sl], S, Cf, kind)
+        counts = torch.stack([n[0] for _, _, n in views])
+        gcounts, gsums = _sync_stats(torch.stack(_fdl_record_sums(views)), counts)
+        fdc = _fdl_total(views, gcounts, world, 1.5)
+        fdc.backward()
+        ga, gb = wa.grad.clone(), wb.grad.clone()
+        D.allreduce_(ga)
+        D.allreduce_(gb)
+        rec = _fdl_record(views, gsums, gcounts, world, 1.5)
+        q.put((rank, ga.tolist(), gb.tolist(), float(rec)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["cov", "dist"])
+def test_dp_fdl_matches_single_process(kind):
+    """FDL under data parallelism: a covariance view is a MEAN over
+    each rank's rows; _fdl_total rescales it by n_loc / N_glob so the SUM
+    all-reduced gradient and the record equal one device running the global
+    batch (projects/MT_UBPL.py:301-330), also with unequal labeled rows per rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fdl_worker, args=(r, 2, port, q, kind)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from ubpl_amd.train import _fdl_record, _fdl_total
+    x, isl, wa0, wb0, (S, Cf) = _fdl_data()
+    wa, wb = wa0.clone().requires_grad_(True), wb0.clone().requires_grad_(True)
+    views = _fdl_local_views(wa, wb, x, isl, S, Cf, kind)
+    counts = torch.stack([n[0] for _, _, n in views])
+    # the reference: fdc = W * sum_a value_a / sum_a n_a on one device
+    ref = 1.5 * sum(v for _, v, _ in views) / counts.sum()
+    ref.backward()
+    ours = _fdl_total(views, counts, 1, 1.5)
+    assert abs(float(ours) - float(ref)) <= 1e-6 * abs(float(ref))
+    rec1 = _fdl_record(views, None, counts, 1, 1.5)
+    assert abs(float(rec1) - float(ref)) <= 1e-6 * abs(float(ref))
+    for rank, ga, gb, rec in res:
+        torch.testing.assert_close(torch.tensor(ga), wa.grad, rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(torch.tensor(gb), wb.grad, rtol=1e-5, atol=1e-7)
+        assert abs(rec - float(ref)) <= 1e-5 * abs(float(ref)), (rec, float(ref))
+
+
 def test_single_process_helpers_are_identity():
     from ubpl_amd import dist as D
     from ubpl_amd.train import _sync_stats

@@ -85,7 +85,8 @@ def _our_grads(model):
     return {n: (None if p.grad is None else p.grad.detach().cpu()) for n, p in model.named_parameters()}
 
 
-@pytest.mark.parametrize("case", list(seeds.hg_cases().keys()))
+@pytest.mark.parametrize("case", [pytest.param(c, marks=pytest.mark.timeout(600)) if c == "hg8_384" else c
+                                  for c in seeds.hg_cases()])
 def test_hourglass_vs_golden(case):
     from ubpl_amd.hourglass import StackedHourglass
     g = np.load(os.path.join(GD, "hourglass.npz"))

@@ -2,13 +2,21 @@
 
 The models, optimisers and batch are built exactly as the reference's main()
 builds them (seeds.step_models / step_batch; tests/golden/gen_golden.py ran
-the reference's own train() on the same inputs).  Checked:
-* the returned records (pec/mtc/epc/fdc averages): 1e-3 relative to golden;
+the reference's own train() on the same inputs, steps.npz).  The exact result
+is the oracle's restatement run in float64 (gen_oracle64.py, steps64.npz).
+Checked, per case:
+* the returned records (pec/mtc/epc/fdc averages) and every student
+  parameter's gradient as the optimizer sees it (norm, sum and 8 sampled
+  elements) — by MAGNITUDE, with the criterion of test_gpu_hourglass.py:
+  |ours - fp64| <= 3 |reference fp32 - fp64| + 1e-4 |fp64| (the reference's
+  own fp32 step sits up to a few % from exact on deep train-mode BN
+  gradients at B=4, SURVEY Appendix A / DESIGN §2).  A lost loss weight, a
+  single instead of doubled FDL gradient (projects/MT_UBPL.py:334-336) or a
+  wrong normaliser moves these by O(1);
 * the per-batch printed counts (n_sel, n_pseudo): exact;
-* AdamW's first step moves each weight by ~ -lr*sign(grad): the update signs
-  agree with the oracle's step (run here on the CPU) on >= 97 % of each
-  student's weights and >= 90 % of every tensor (grads whose sign is below fp32 noise can flip — the
-  reference's own fp32 gradients are ~2 % from exact, see test_gpu_hourglass);
+* the parameter update: per tensor, the sum of (p1 - p0)/lr (AdamW's first
+  step is ~sign(g) per element) within a few noise-signed elements of the
+  reference's;
 * teachers after the EMA update equal alpha*teacher + (1-alpha)*student
   (alpha keyed on the epoch) to fp32 rounding;
 * BN running statistics: 1e-3 relative.
@@ -20,9 +28,7 @@ import pytest
 import torch
 
 import seeds
-from oracle import hourglass as OH
 from oracle import render as OR
-from oracle import step as OS
 
 pytestmark = pytest.mark.gpu
 GD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -42,7 +48,9 @@ def _factory(k, s, mode):
     return StackedHourglass(k, s, mode)
 
 
-def _run_ours(cfg, flat_adam):
+def _run_ours(cfg, flat_adam, monkeypatch):
+    """Our train() on the case; also returns each student's gradient record as
+    its optimizer step sees it."""
     from ubpl_amd import train as T
     from ubpl_amd.optim import FlatAdamW
     models, emas, optims = seeds.step_models(_factory, cfg, device="cuda")
@@ -50,8 +58,20 @@ def _run_ours(cfg, flat_adam):
         optims = [FlatAdamW(m, lr=cfg["lr"], weight_decay=0) for m in models]
     before = [[p.detach().clone() for p in m.parameters()] for m in models + emas]
     loader, args = seeds.step_batch(cfg, OR.kps_heatmap_torch)
+    grads = {}
+
+    def snap():
+        torch.cuda.synchronize()
+        for mi, m in enumerate(models):
+            grads[mi] = seeds.grad_record([(n, p.grad) for n, p in m.named_parameters()])
+    orig = T._step_and_ema
+    monkeypatch.setattr(T, "_step_and_ema", lambda *a, **k: (snap(), orig(*a, **k))[1])
+    for o in optims:
+        ostep = o.step
+        o.step = lambda *a, _s=ostep, **k: (snap() if not grads else None, _s(*a, **k))[1]
     import io
     import contextlib
+    import re
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
         if cfg["project"] == "MT_UBPL":
@@ -62,67 +82,78 @@ def _run_ours(cfg, flat_adam):
             rec = T.train_mt(loader, models[0], emas[0], optims[0], args)
         else:
             rec = T.train_supervised(loader, models[0], optims[0], args)
-    import re
     counts = [[int(a), int(b)] for a, b in re.findall(r"\((\s*\d+)/(\s*\d+)\)", buf.getvalue())]
-    return models + emas, before, rec, counts, args
+    return models + emas, before, rec, counts, args, grads
 
 
-def _run_oracle(cfg):
-    models, emas, optims = seeds.step_models(OH.oracle_factory, cfg)
-    before = [[p.detach().clone() for p in m.parameters()] for m in models + emas]
-    loader, args = seeds.step_batch(cfg, OR.kps_heatmap_torch)
-    if cfg["project"] == "MT_UBPL":
-        OS.train_mt_ubpl(loader, models, emas, optims, args)
-    elif cfg["project"] == "DualPose_UBPL":
-        OS.train_dualpose_ubpl(loader, models, emas, optims, args)
-    elif cfg["project"] == "MT":
-        OS.train_mt(loader, models[0], emas[0], optims[0], args)
-    else:
-        OS.train_supervised(loader, models[0], optims[0], args)
-    return models + emas, before
+def _noise_floor(ours, ref32, ref64, scale, rtol=1e-4):
+    """|ours - fp64| <= 3 |ref32 - fp64| + rtol * scale (elementwise)."""
+    return np.abs(ours - ref64) <= 3 * np.abs(ref32 - ref64) + rtol * scale + 1e-12
 
 
-@pytest.mark.parametrize("case,flat_adam", [("mt_ubpl", True), ("mt_ubpl_e0", False), ("dualpose", True),
-                                            ("mt", True), ("sup", False)])
-def test_train_step_vs_reference(case, flat_adam):
-    torch.set_num_threads(min(32, os.cpu_count() or 1))
+def check_step_grads(case, mi, rec, names, g32, g64):
+    st, sa = rec
+    st32, sa32 = g32[case + "/model%d/grad_stats" % mi], g32[case + "/model%d/grad_samp" % mi]
+    st64, sa64 = g64[case + "/model%d/grad_stats" % mi], g64[case + "/model%d/grad_samp" % mi]
+    live = st64[:, 1] > 0
+    keep = np.array([not seeds.bn_cancelled(n) for n in names])
+    assert np.array_equal((st[:, 1] > 0)[keep], live[keep]), (case, mi)
+    bad = []
+    for i, n in enumerate(names):
+        if not live[i] or seeds.bn_cancelled(n):
+            continue
+        n64, n32, no = np.sqrt(st64[i, 1]), np.sqrt(st32[i, 1]), np.sqrt(st[i, 1])
+        ok_n = _noise_floor(no, n32, n64, n64)
+        s64, s32, so = sa64[i], sa32[i], sa[i]
+        m = ~np.isnan(s64)
+        ok_s = _noise_floor(so[m], s32[m], s64[m], np.abs(s64[m]).max()).all()
+        # the sum carries the sign pattern; its scale is the sum of |g|
+        ok_sum = _noise_floor(st[i, 0], st32[i, 0], st64[i, 0], st64[i, 2])
+        if not (ok_n and ok_s and ok_sum):
+            bad.append((n, float(no / n64 - 1), float(n32 / n64 - 1), bool(ok_s), bool(ok_sum)))
+    assert not bad, (case, mi, len(bad), bad[:6])
+
+
+STEP_CASES = [("mt_ubpl", True), ("mt_ubpl_e0", False), ("dualpose", True), ("mt", True), ("sup", False),
+              ("mt_ubpl_noep", True), ("dualpose_hg4", True), ("mt_ubpl_b32", True)]
+
+
+@pytest.mark.parametrize("case,flat_adam", STEP_CASES)
+def test_train_step_vs_reference(case, flat_adam, monkeypatch):
     g = np.load(os.path.join(GD, "steps.npz"))
+    g64 = np.load(os.path.join(GD, "steps64.npz"))
     cfg = seeds.step_cases()[case]
-    ours, before, rec, counts, args = _run_ours(cfg, flat_adam)
-    np.testing.assert_allclose(_flat(rec, []), g[case + "/records"], rtol=1e-3, atol=1e-9)
+    ours, before, rec, counts, args, grads = _run_ours(cfg, flat_adam, monkeypatch)
+    r, r32, r64 = np.array(_flat(rec, [])), g[case + "/records"], g64[case + "/records"]
+    assert _noise_floor(r, r32, r64, np.abs(r64)).all(), (r, r32, r64)
     assert np.array_equal(np.array(counts, np.int64).reshape(-1, 2), g[case + "/printed_counts"])
-    ref, ref_before = _run_oracle(cfg)
     n_students = cfg["brNum"]
-    for mi, (m, r, b0, rb0) in enumerate(zip(ours, ref, before, ref_before)):
-        names = [n for n, _ in m.named_parameters()]
-        agree_n, total_n = 0, 0
-        for n, p, q, p0, q0 in zip(names, m.parameters(), r.parameters(), b0, rb0):
-            assert torch.equal(p0.cpu(), q0), (mi, n)          # same seeded init
-            du = (p.detach().cpu() - p0.cpu()).double()
-            dr = (q.detach() - q0).double()
-            if mi < n_students:
-                if seeds.bn_cancelled(n) or float(dr.abs().max()) == 0.0:
-                    assert float(du.abs().max()) <= 1.01 * args.lr, (mi, n)
-                    continue
-                same = int(((du > 0) == (dr > 0)).sum())
-                agree_n, total_n = agree_n + same, total_n + du.numel()
-                assert same >= 0.9 * du.numel(), (mi, n, same / du.numel())
-            else:
-                # teacher = alpha*teacher + (1-alpha)*student_after_step (utils/parameters.py:6-8),
-                # checked on our own tensors (the students were checked against the oracle above)
-                s_new = dict(ours[mi - len(ours) // 2].named_parameters())[n].detach().cpu()
+    names = [n for n, _ in ours[0].named_parameters()]
+    for mi in range(n_students):
+        check_step_grads(case, mi, grads[mi], names, g, g64)
+    for mi, (m, b0) in enumerate(zip(ours, before)):
+        if mi < n_students:
+            upd = np.array([((p.detach().cpu().double() - q.cpu().double()) / args.lr).sum().item()
+                            for p, q in zip(m.parameters(), b0)])
+            ref, absu = g[case + "/model%d/upd" % mi], g[case + "/model%d/absupd" % mi]
+            noisy = np.array([seeds.bn_cancelled(n) for n in names])
+            bad = (np.abs(upd - ref) > 1e-3 * absu + 6.0) & ~noisy
+            assert not bad.any(), (mi, [names[i] for i in np.nonzero(bad)[0]][:8])
+        else:
+            # teacher = alpha*teacher + (1-alpha)*student_after_step (utils/parameters.py:6-8)
+            for n, p, p0 in zip(names, m.parameters(), b0):
+                s_new = dict(ours[mi - n_students].named_parameters())[n].detach().cpu()
                 alpha = min(1 - 1 / (args.epo + 1), args.ema_decay)
                 a_part, b_part = p0.cpu().double() * alpha, (1 - alpha) * s_new.double()
                 err = (p.detach().cpu().double() - (a_part + b_part)).abs()
                 assert bool((err <= 2.5e-7 * (a_part.abs() + b_part.abs()) + 1e-12).all()), (mi, n)
-        if mi < n_students:
-            assert agree_n >= 0.97 * total_n, (mi, agree_n / total_n)
-        for (bn, b), (_, rb) in zip(m.named_buffers(), r.named_buffers()):
-            if bn.endswith("num_batches_tracked"):
-                assert int(b) == int(rb), bn
-            else:
-                err = float((b.cpu().double() - rb.double()).norm() / (rb.double().norm() + 1e-30))
-                assert err < 1e-3, (mi, bn, err)
+        bst = np.array([[b.detach().double().sum().item(), (b.detach().double() ** 2).sum().item()]
+                        for _, b in m.named_buffers()])
+        ref = g[case + "/model%d/buf" % mi]
+        assert np.array_equal(bst[2::3], ref[2::3])                          # num_batches_tracked
+        nb, nr = np.sqrt(bst[:, 1]), np.sqrt(ref[:, 1])                      # per-buffer norms
+        err = np.abs(nb - nr) <= 1e-3 * nr + 1e-7
+        assert err.all(), (mi, np.argwhere(~err)[:4])
 
 
 def test_step_graph_replay_matches_eager(monkeypatch):

@@ -99,6 +99,58 @@ def _norm(s, n):
     return torch.where(n > 0, s / n.clamp(min=1.0), s)
 
 
+def _fdl_view(fa, fb, rowmask, args):
+    """One view of the multi-view feature decorrelation term (projects/MT_UBPL.py:
+    301-330, DualPose_UBPL.py:246-270) over the selected rows (rowmask > 0):
+    returns (kind, value, n_loc) with n_loc a device float[1].
+
+    'covariance' (FDL_type default): value = ProcessUtils.features_cov of the
+    selected rows = their MEAN |cov| (0 when no row of this rank is selected),
+    n_loc = rows * S * C.  Any other FDL_type: the reference's else branch,
+    JointFeatureDistLoss (utils/losses.py:56-70): value = SUM over the selected
+    (sample, stack, channel) rows of the pixel-mean squared distance, n_loc =
+    rows * S.  The value of a covariance view is a mean, so under data
+    parallelism _fdl_total rescales it by n_loc / N_glob before summing."""
+    if args.FDL_type == "covariance":
+        v, c = features_cov(fa, fb, rowmask)
+        n = c.float()
+        return "cov", torch.where(n[0] > 0, v, torch.zeros_like(v)), n
+    B, S, C = fa.shape[:3]
+    HW = fa[0, 0, 0].numel()
+    spec = (0, 1, S * C, HW, (S * C * HW, 0, 0, 1), False, True, 0.0)
+    s, _, _ = _RowLoss.apply(fa.contiguous(), fb.contiguous(), spec, None, rowmask.reshape(-1).contiguous())
+    return "dist", s, ((rowmask > 0).sum() * S).float().reshape(1)
+
+
+def _fdl_total(views, gcounts_v, W, weight):
+    """fdc = FDLWeight * (sum_a value_a) / (sum_a N_a) with global counts N_a
+    (MT_UBPL.py:329).  A covariance view is a mean over this rank's rows;
+    value_a * n_loc_a / N_a is its share of the global-batch mean (exactly
+    value_a on one rank), so the SUM all-reduce of the gradients gives the
+    single-device gradient."""
+    terms = []
+    for (kind, v, n_loc), N_a in zip(views, gcounts_v):
+        if kind == "cov" and W > 1:
+            v = v * (n_loc[0] / N_a.clamp(min=1.0))
+        terms.append(v)
+    return weight * _norm(sum(terms), sum(gcounts_v))
+
+
+def _fdl_record_sums(views):
+    """What each rank contributes to the all-reduced FDL record: the local
+    SUM (covariance: mean * rows)."""
+    return [v.detach() * n[0] if kind == "cov" else v.detach() for kind, v, n in views]
+
+
+def _fdl_record(views, gsums_v, gcounts_v, W, weight):
+    if W == 1:
+        vals = [v.detach() for _, v, _ in views]
+    else:
+        vals = [s / N.clamp(min=1.0) if kind == "cov" else s
+                for (kind, _, _), s, N in zip(views, gsums_v, gcounts_v)]
+    return weight * _norm(sum(vals), sum(gcounts_v))
+
+
 def _islabeled(meta_isl, dev):
     return meta_isl.to(dev, non_blocking=True).reshape(-1)
 
@@ -300,6 +352,11 @@ class _StepGraph:
         streams = len(models) >= 2 and os.environ.get("UBPL_MODEL_STREAMS", "1") != "0"
         want = (env == "1") if env is not None else not streams
         self.enabled = want and not D.is_dist() and all(hasattr(o, "_step_t") for o in optims)
+        if self.enabled and streams:
+            import warnings
+            warnings.warn("ubpl_amd: UBPL_STEP_GRAPH=1 with per-network streams: the captured step is not "
+                          "bit-identical to the eager step (DESIGN.md §6)", RuntimeWarning)
+        self.hkey = None
         self.n_eager = 0
         self.graph = None
         self.key = None
@@ -327,13 +384,36 @@ class _StepGraph:
 
     @classmethod
     def get(cls, core, models, models_ema, optims, args):
-        akey = repr(sorted(vars(args).items())) if hasattr(args, "__dict__") else repr(args)
-        okey = repr([o.param_groups for o in optims])
-        key = (core.__name__, tuple(map(id, models)), tuple(map(id, models_ema)), tuple(map(id, optims)), akey,
-               okey)
-        if key not in cls._cache:
-            cls._cache[key] = cls(core, models, models_ema, optims, args)
-        return cls._cache[key]
+        """One runner per (step function, networks, optimisers).  The host
+        constants the captured step bakes in (args: loss weights, epoch ->
+        EMA alpha; the learning rates) change every epoch: then the old graph
+        and its memory pool are released and the next step re-captures."""
+        key = (core.__name__, tuple(map(id, models)), tuple(map(id, models_ema)), tuple(map(id, optims)))
+        hkey = (repr(sorted(vars(args).items())) if hasattr(args, "__dict__") else repr(args),
+                repr([o.param_groups for o in optims]))
+        r = cls._cache.get(key)
+        if r is None:
+            cls.clear()                      # one runner: an old one would pin its networks and pool
+            r = cls._cache[key] = cls(core, models, models_ema, optims, args)
+            r.hkey = hkey
+        if r.hkey != hkey:
+            r.release()
+            r.args, r.hkey = args, hkey
+        return r
+
+    @classmethod
+    def clear(cls):
+        for r in cls._cache.values():
+            r.release()
+        cls._cache.clear()
+
+    def release(self):
+        """Drop the captured graph, its static inputs and outputs (its private
+        memory pool goes with them)."""
+        if self.graph is not None:
+            self.graph.reset()
+            self.graph, self.key, self.static, self.out = None, None, None, None
+            torch.cuda.empty_cache()
 
     def _eager(self, batch):
         return self.core(self.models, self.emas, self.optims, self.args, *batch)
@@ -415,48 +495,50 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
         outs = [[_OnMain.apply(t) for t in ts] for ts in outs]
         feats = [[None if t is None else _OnMain.apply(t) for t in ts] for ts in feats]
     K = outs[0][0].shape[2]
+    use_ep = getattr(args, "useEnsemblePseudo", True)        # :271 (False: epc = 0, no print)
+    zero = torch.zeros((), device=dev)
+    zcnt = torch.zeros(4, dtype=torch.int32, device=dev)
     # ---- loss sums / counts on device
-    sums, cnts = [], []
+    sums = []
     ps_scores = []
     for mi in range(M):
         ms = []
         for a in range(A):
             s_d, _ = _dist_last(outs[mi][a], outs_ema[mi][a])
             s_p, c_p = _mse(outs[mi][a], hms[a], S, gates[a], sw.reshape(-1, 1))
-            tg = torch.stack([outs_ema[j][a] for j in range(M)])
-            s_e, c_e, sc_e = _pseudo(outs[mi][a], tg, nega, S, args.pseudoScoreThr)
+            if use_ep:
+                tg = torch.stack([outs_ema[j][a] for j in range(M)])
+                s_e, c_e, sc_e = _pseudo(outs[mi][a], tg, nega, S, args.pseudoScoreThr)
+                ps_scores.append(sc_e)
+            else:
+                s_e, c_e = zero, zcnt
             ms.append((s_d, s_p, c_p, s_e, c_e))
-            ps_scores.append(sc_e)
         sums.append(ms)
     fd = []
     if args.FDLWeight > 0:
-        for a in range(A):                                   # :301-330 labeled rows
-            rowmask = _fdl_rows(sw, args)
-            v, c = features_cov(feats[0][a], feats[1][a], rowmask)
-            fd.append((v, c))
-    # pack: per model [mtc_sum, pec_sum, epc_sum], counts [pec_n, epc_n, n_sel] ; fdc
+        rowmask = _fdl_rows(sw, args)
+        for a in range(A):                                   # :301-330 selected rows
+            fd.append(_fdl_view(feats[0][a], feats[1][a], rowmask, args))
+    # pack: per model [mtc_sum, pec_sum, epc_sum], counts [pec_n, epc_n, n_sel]; per FDL view sum / count
     loc = []
     cn = []
     for mi in range(M):
         loc += [sum(x[0] for x in sums[mi]), sum(x[1] for x in sums[mi]), sum(x[3] for x in sums[mi])]
         cn += [sum(x[2][0] for x in sums[mi]), sum(x[4][1] for x in sums[mi]), sum(x[4][2] for x in sums[mi])]
-    if fd:
-        loc.append(sum(v for v, _ in fd))
-        cn.append(sum(c[0] for _, c in fd))
+    loc += _fdl_record_sums(fd)
+    cn += [n[0] for _, _, n in fd]
     counts = torch.stack([c.float() for c in cn])
     gcounts, gsums = _sync_stats(torch.stack([l.float() for l in loc]), counts)
     W = D.world()
     mtc_n = A * B * K * W
-    totals, rec = [], []
-    fdc = 0.
-    if fd:
-        fdc = args.FDLWeight * _norm(loc[-1], gcounts[-1])
+    nf = len(fd)
+    totals = []
+    fdc = _fdl_total(fd, gcounts[3 * M:], W, args.FDLWeight) if fd else 0.
     for mi in range(M):
         mtc = args.consWeight * (loc[3 * mi] / mtc_n)
         pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[3 * mi])
-        epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[3 * mi + 1])
+        epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[3 * mi + 1]) if use_ep else 0.
         totals.append(pec + mtc + epc + fdc)
-        rec.append((pec, mtc, epc))
     _backward_all(totals)                                     # :334-336
     if mstreams:
         mstreams.join()
@@ -469,11 +551,11 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
     for mi in range(M):
         g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[3 * mi]),
                   args.consWeight * gsums[3 * mi] / mtc_n,
-                  args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[3 * mi + 1])]
-    g_rec.append(args.FDLWeight * _norm(gsums[-1], gcounts[-1]) if fd else torch.zeros((), device=dev))
-    score = torch.stack(ps_scores).mean(0)
+                  args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[3 * mi + 1]) if use_ep else zero]
+    g_rec.append(_fdl_record(fd, gsums[3 * M:], gcounts[3 * M:], W, args.FDLWeight) if fd else zero)
+    score = torch.stack(ps_scores).mean(0) if use_ep else torch.zeros(K, device=dev)
     packed = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, score])
-    return packed, (bool(fd), mtc_n, B, len(cn))
+    return packed, (nf, mtc_n, B, len(cn), use_ep)
 
 
 def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
@@ -492,18 +574,19 @@ def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
         e.train()
     runner = _StepGraph.get(_mt_ubpl_core, models, models_ema, optims, args)
     for bat, (augs_imgMap, augs_heatmaps, meta) in enumerate(trainLoader):
-        packed, (fd, mtc_n, B, ncn) = runner.run((augs_imgMap, augs_heatmaps, meta), dev)
+        packed, (nf, mtc_n, B, ncn, use_ep) = runner.run((augs_imgMap, augs_heatmaps, meta), dev)
         host = packed.cpu().tolist()                              # the step's one device->host copy
         nrec = 3 * M + 1
         for mi in range(M):
             pec_c[mi].update(host[3 * mi], int(host[nrec + 3 * mi]))
             mtc_c[mi].update(host[3 * mi + 1], mtc_n)
-            epc_c[mi].update(host[3 * mi + 2], int(host[nrec + 3 * mi + 1]))
-        if fd:
-            fdc_c.update(host[3 * M], int(host[nrec + 3 * M]))
+            # useEnsemblePseudo False: epc_counter.update(0., outs.shape[2]) (:292-293; outs.shape[2] = B)
+            epc_c[mi].update(host[3 * mi + 2], int(host[nrec + 3 * mi + 1]) if use_ep else B)
+        if nf:
+            fdc_c.update(host[3 * M], int(sum(host[nrec + 3 * M:nrec + 3 * M + nf])))
         else:
             fdc_c.update(0., B)
-        if verbose:
+        if verbose and use_ep:
             n_ps = int(sum(host[nrec + 3 * mi + 1] for mi in range(M)))
             n_sel = int(sum(host[nrec + 3 * mi + 2] for mi in range(M)))
             sc = host[nrec + ncn:]
@@ -555,60 +638,77 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
         nega = _w(isl, 0.0, args.pseudoWeight)
         cons = _w(isl, 1.0, args.pseudoWeight)
         B = si.shape[0]
-        outs, feats = [], []
-        for mi in range(M):
-            o, f = models[mi](si)
+        outs, feats, ema_l = [], [], []
+        mstreams = _ModelStreams.make(M, dev)                    # one HIP stream per network
+        for mi in range(M):                                       # :185-196
+            with (mstreams.on(mi) if mstreams else contextlib.nullcontext()):
+                o, f = models[mi](si)
             outs.append(o)
             feats.append(f)
-        with torch.no_grad():
-            outs_ema = torch.stack([models_ema[mi](ei)[0] for mi in range(M)])
+            with (mstreams.on_teacher(mi) if mstreams else contextlib.nullcontext()), torch.no_grad():
+                ema_l.append(models_ema[mi](ei)[0])
+        if mstreams:
+            mstreams.join(outs + feats + ema_l)
+            outs = [_OnMain.apply(t) for t in outs]
+            feats = [None if t is None else _OnMain.apply(t) for t in feats]
+        outs_ema = torch.stack(ema_l)
+        use_ep = getattr(args, "useEnsemblePseudo", True)    # :224 (False: epc = 0, no print)
+        K = outs[0].shape[2]
+        zero = torch.zeros((), device=dev)
         loc, cn, cons_sc, ps_sc = [], [], [], []
         for mi in range(M):
             s_c, c_c, sc_c = _dist_mt2_last(outs[mi], outs_ema[mi], cons, args.pseudoScoreThr)
             s_p, c_p = _mse(outs[mi], hm, S, gate, sw.reshape(-1, 1))
-            s_e, c_e, sc_e = _pseudo(outs[mi], outs_ema, nega, S, args.pseudoScoreThr)
+            if use_ep:
+                s_e, c_e, sc_e = _pseudo(outs[mi], outs_ema, nega, S, args.pseudoScoreThr)
+                ps_sc.append(sc_e)
+            else:
+                s_e, c_e = zero, torch.zeros(4, dtype=torch.int32, device=dev)
             loc += [s_c, s_p, s_e]
             cn += [c_c[0], c_p[0], c_e[1], c_c[1], c_c[2], c_e[2]]
             cons_sc.append(sc_c)
-            ps_sc.append(sc_e)
-        fd = None
-        if args.FDLWeight > 0:
-            fd = features_cov(feats[0], feats[1], _fdl_rows(sw, args))
-            loc.append(fd[0])
-            cn.append(fd[1][0])
+        fd = []
+        if args.FDLWeight > 0:                                     # :246-270 (one view)
+            fd.append(_fdl_view(feats[0], feats[1], _fdl_rows(sw, args), args))
+        loc += _fdl_record_sums(fd)
+        cn += [n[0] for _, _, n in fd]
         counts = torch.stack([c.float() for c in cn])
         gcounts, gsums = _sync_stats(torch.stack([l.float() for l in loc]), counts)
-        fdc = args.FDLWeight * _norm(fd[0], gcounts[-1]) if fd is not None else 0.
+        W = D.world()
+        fdc = _fdl_total(fd, gcounts[6 * M:], W, args.FDLWeight) if fd else 0.
         totals = []
         for mi in range(M):
             mtc = args.consWeight * _norm(loc[3 * mi], gcounts[6 * mi])
             pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[6 * mi + 1])
-            epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2])
+            epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else 0.
             totals.append(pec + mtc + epc + fdc)
         _backward_all(totals)                                     # DualPose_UBPL.py:277-279
+        if mstreams:
+            mstreams.join()
+        for m in models:
+            m.merge_alt_grads()
         D.allreduce_grads(models)
         _step_and_ema(models, models_ema, optims, args)
         g_rec = []
         for mi in range(M):
             g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[6 * mi + 1]),
                       args.consWeight * _norm(gsums[3 * mi], gcounts[6 * mi]),
-                      args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[6 * mi + 2])]
-        g_rec.append(args.FDLWeight * _norm(gsums[-1], gcounts[-1]) if fd is not None else
-                     torch.zeros((), device=dev))
+                      args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else zero]
+        g_rec.append(_fdl_record(fd, gsums[3 * M:], gcounts[6 * M:], W, args.FDLWeight) if fd else zero)
         host = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, torch.stack(cons_sc).mean(0),
-                          torch.stack(ps_sc).mean(0)]).cpu().tolist()
+                          torch.stack(ps_sc).mean(0) if use_ep else torch.zeros(K, device=dev)]).cpu().tolist()
         nrec = 3 * M + 1
         cbase = nrec
         for mi in range(M):
             pec_c[mi].update(host[3 * mi], int(host[cbase + 6 * mi + 1]))
             mtc_c[mi].update(host[3 * mi + 1], int(host[cbase + 6 * mi]))
-            epc_c[mi].update(host[3 * mi + 2], int(host[cbase + 6 * mi + 2]))
-        if fd is not None:
+            # useEnsemblePseudo False: epc_counter.update(0., outs.shape[2]) (:244-245; outs.shape[2] = nStack)
+            epc_c[mi].update(host[3 * mi + 2], int(host[cbase + 6 * mi + 2]) if use_ep else S)
+        if fd:
             fdc_c.update(host[3 * M], int(host[cbase + 6 * M]))
         else:
-            fdc_c.update(0., B)
+            fdc_c.update(0., S)                                   # :249 outs.shape[2] = nStack
         if verbose:
-            K = outs[0].shape[2]
             off = cbase + len(cn)
             c_ps = int(sum(host[cbase + 6 * mi + 3] for mi in range(M)))
             c_sel = int(sum(host[cbase + 6 * mi + 4] for mi in range(M)))
@@ -618,10 +718,11 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
                 format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
                 format(c_sel / c_ps if c_ps else float("nan"), ".2f"), format(c_sel, "5d"), format(c_ps, "5d"),
                 ", ".join(format(v, ".3f") for v in host[off:off + K])))
-            print("batch.{} ensemble-pseudo (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
-                format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
-                format(e_sel / e_ps if e_ps else float("nan"), ".2f"), format(e_sel, "5d"), format(e_ps, "5d"),
-                ", ".join(format(v, ".3f") for v in host[off + K:off + 2 * K])))
+            if use_ep:
+                print("batch.{} ensemble-pseudo (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
+                    format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
+                    format(e_sel / e_ps if e_ps else float("nan"), ".2f"), format(e_sel, "5d"), format(e_ps, "5d"),
+                    ", ".join(format(v, ".3f") for v in host[off + K:off + 2 * K])))
         del outs, outs_ema, feats, totals
     return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
 
