@@ -234,6 +234,10 @@ def step_cases():
         "mt_ubpl_noep": dict(base, project="MT_UBPL", S=2, K=16, B=4, nlab=2, epo=1, consWeight=3.0,
                              thr=0.15, mode="AvgPool", brNum=2, A=2, seed=606, useEnsemblePseudo=False,
                              FDL_type="distance"),
+        # FDL weighted up so its gradient is a sizeable part of every student's: pins the
+        # doubled FDL gradient (fdc in both totals, projects/MT_UBPL.py:334-336) by magnitude
+        "mt_ubpl_fdl": dict(base, project="MT_UBPL", S=2, K=16, B=4, nlab=2, epo=1, consWeight=3.0,
+                            thr=0.15, mode="AvgPool", brNum=2, A=2, seed=609, FDLWeight=2.0e4),
         # BASELINE.json configs[3]: DualPose_UBPL, dual 4-stack hourglasses, K=17
         "dualpose_hg4": dict(base, project="DualPose_UBPL", S=4, K=17, B=4, nlab=2, epo=3, consWeight=5.0,
                              thr=0.15, mode="AvgPool", brNum=2, A=1, seed=607, pseudoWeight=0.5),

@@ -91,31 +91,45 @@ def _noise_floor(ours, ref32, ref64, scale, rtol=1e-4):
     return np.abs(ours - ref64) <= 3 * np.abs(ref32 - ref64) + rtol * scale + 1e-12
 
 
+def _grad_errors(st, sa, st64, sa64, idx):
+    """Per-parameter relative errors against fp64 of a gradient record: the
+    norm, the 8 sampled elements (L2) and the sum (relative to sum |g|)."""
+    e = []
+    for i in idx:
+        m = ~np.isnan(sa64[i])
+        n64 = np.sqrt(st64[i, 1])
+        e.append((abs(np.sqrt(st[i, 1]) - n64) / n64,
+                  np.linalg.norm(sa[i][m] - sa64[i][m]) / max(np.linalg.norm(sa64[i][m]), 1e-30),
+                  abs(st[i, 0] - st64[i, 0]) / max(st64[i, 2], 1e-30)))
+    return np.array(e)
+
+
 def check_step_grads(case, mi, rec, names, g32, g64):
+    """Our gradients vs fp64, against the reference's fp32 gradients vs fp64.
+    Per-parameter errors of fp32 gradients are random (one realisation per
+    tensor), so the bar is statistical over the ~450 tensors of a student:
+    median and 95th percentile no worse than 2x / 3x the reference's, and no
+    tensor beyond 3x its own reference error + 10x the reference's median
+    error (a lost factor or term moves tensors by 10-100 %)."""
     st, sa = rec
     st32, sa32 = g32[case + "/model%d/grad_stats" % mi], g32[case + "/model%d/grad_samp" % mi]
     st64, sa64 = g64[case + "/model%d/grad_stats" % mi], g64[case + "/model%d/grad_samp" % mi]
     live = st64[:, 1] > 0
     keep = np.array([not seeds.bn_cancelled(n) for n in names])
     assert np.array_equal((st[:, 1] > 0)[keep], live[keep]), (case, mi)
-    bad = []
-    for i, n in enumerate(names):
-        if not live[i] or seeds.bn_cancelled(n):
-            continue
-        n64, n32, no = np.sqrt(st64[i, 1]), np.sqrt(st32[i, 1]), np.sqrt(st[i, 1])
-        ok_n = _noise_floor(no, n32, n64, n64)
-        s64, s32, so = sa64[i], sa32[i], sa[i]
-        m = ~np.isnan(s64)
-        ok_s = _noise_floor(so[m], s32[m], s64[m], np.abs(s64[m]).max()).all()
-        # the sum carries the sign pattern; its scale is the sum of |g|
-        ok_sum = _noise_floor(st[i, 0], st32[i, 0], st64[i, 0], st64[i, 2])
-        if not (ok_n and ok_s and ok_sum):
-            bad.append((n, float(no / n64 - 1), float(n32 / n64 - 1), bool(ok_s), bool(ok_sum)))
-    assert not bad, (case, mi, len(bad), bad[:6])
+    idx = [i for i in range(len(names)) if live[i] and keep[i]]
+    eo, er = _grad_errors(st, sa, st64, sa64, idx), _grad_errors(st32, sa32, st64, sa64, idx)
+    for c, what in enumerate(("norm", "samples", "sum")):
+        mo, mr = np.median(eo[:, c]), np.median(er[:, c])
+        po, pr = np.percentile(eo[:, c], 95), np.percentile(er[:, c], 95)
+        assert mo <= 2 * mr + 1e-5, (case, mi, what, "median", mo, mr)
+        assert po <= 3 * pr + 1e-4, (case, mi, what, "p95", po, pr)
+        bad = np.nonzero(eo[:, c] > 3 * er[:, c] + 10 * mr + 1e-4)[0]
+        assert bad.size == 0, (case, mi, what, [(names[idx[b]], eo[b, c], er[b, c]) for b in bad[:5]])
 
 
 STEP_CASES = [("mt_ubpl", True), ("mt_ubpl_e0", False), ("dualpose", True), ("mt", True), ("sup", False),
-              ("mt_ubpl_noep", True), ("dualpose_hg4", True), ("mt_ubpl_b32", True)]
+              ("mt_ubpl_noep", True), ("mt_ubpl_fdl", True), ("dualpose_hg4", True), ("mt_ubpl_b32", True)]
 
 
 @pytest.mark.parametrize("case,flat_adam", STEP_CASES)
