@@ -117,13 +117,13 @@ class PsaLaunches:
         behind a spin kernel so no host gap enters the window) between two HIP
         events on the stream they were launched on; returns the average
         duration of one launch in ms."""
-        fn = self.lib.lib().ubpl_conv2d_forward_psa
+        fn = self.lib.op("ubpl_conv2d_forward_psa")              # the torch op over the C-ABI entry
         calls = [c for c in self.calls if c[14] is None]        # slab pointer: none (no split-K)
         if not calls:
             return None, 0
         torch.cuda.synchronize()
         for c in calls:                                         # warm
-            self.lib.check(fn(*c), "ubpl_conv2d_forward_psa")
+            fn(*c)
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda._sleep(20_000_000)

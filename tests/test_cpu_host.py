@@ -33,6 +33,30 @@ def test_library_exports_every_header_symbol():
     assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
 
 
+def test_torch_ops_mirror_the_header():
+    """libubpl_ops.so registers TORCH_LIBRARY(ubpl): one op per C-ABI entry,
+    device pointers as Tensor? (mutable when the C pointer is), no stream
+    argument (the op uses torch's current stream); host queries run on CPU."""
+    from ubpl_amd import _lib
+    if not os.path.exists(_lib.OPS_PATH):
+        pytest.skip("libubpl_ops.so not built (run __graft_entry__.build())")
+    ops = _lib.load_ops()
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "ubpl_hip.h")).read(), flags=re.S)
+    for ret, name, args in re.findall(r"(int|int64_t)\s+(ubpl_\w+)\s*\(([^;]*?)\)\s*;", txt, flags=re.S):
+        sch = _lib.op(name)._schema
+        params = [a.strip() for a in args.replace("\n", " ").split(",") if a.strip()]
+        c_args = [p for p in params if not p.endswith("stream")]
+        assert len(sch.arguments) == len(c_args), name
+        for a, p in zip(sch.arguments, c_args):
+            if "*" in p:
+                assert str(a.type) == "Optional[Tensor]", (name, p)
+                assert (a.alias_info is not None and a.alias_info.is_write) == (not p.startswith("const")), (name, p)
+            assert a.name == p.split()[-1].lstrip("*"), (name, a.name, p)
+    # a host-only query through its op equals the C-ABI value
+    assert ops.conv2d_forward_psa_workspace(32, 128, 128, 3, 16, 16, 3) == \
+        _lib.lib().ubpl_conv2d_forward_psa_workspace(32, 128, 128, 3, 16, 16, 3)
+
+
 def test_product_fails_loudly_without_gpu():
     if torch.cuda.is_available():
         pytest.skip("GPU present")

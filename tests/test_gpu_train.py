@@ -14,9 +14,7 @@ Checked, per case:
   single instead of doubled FDL gradient (projects/MT_UBPL.py:334-336) or a
   wrong normaliser moves these by O(1);
 * the per-batch printed counts (n_sel, n_pseudo): exact;
-* the parameter update: per tensor, the sum of (p1 - p0)/lr (AdamW's first
-  step is ~sign(g) per element) within a few noise-signed elements of the
-  reference's;
+* the parameter update: AdamW's first step applied to those gradients;
 * teachers after the EMA update equal alpha*teacher + (1-alpha)*student
   (alpha keyed on the epoch) to fp32 rounding;
 * BN running statistics: 1e-3 relative.
@@ -58,12 +56,13 @@ def _run_ours(cfg, flat_adam, monkeypatch):
         optims = [FlatAdamW(m, lr=cfg["lr"], weight_decay=0) for m in models]
     before = [[p.detach().clone() for p in m.parameters()] for m in models + emas]
     loader, args = seeds.step_batch(cfg, OR.kps_heatmap_torch)
-    grads = {}
+    grads, full = {}, {}
 
     def snap():
         torch.cuda.synchronize()
         for mi, m in enumerate(models):
             grads[mi] = seeds.grad_record([(n, p.grad) for n, p in m.named_parameters()])
+            full[mi] = {n: p.grad.detach().double().cpu() for n, p in m.named_parameters() if p.grad is not None}
     orig = T._step_and_ema
     monkeypatch.setattr(T, "_step_and_ema", lambda *a, **k: (snap(), orig(*a, **k))[1])
     for o in optims:
@@ -83,7 +82,7 @@ def _run_ours(cfg, flat_adam, monkeypatch):
         else:
             rec = T.train_supervised(loader, models[0], optims[0], args)
     counts = [[int(a), int(b)] for a, b in re.findall(r"\((\s*\d+)/(\s*\d+)\)", buf.getvalue())]
-    return models + emas, before, rec, counts, args, grads
+    return models + emas, before, rec, counts, args, grads, full
 
 
 def _noise_floor(ours, ref32, ref64, scale, rtol=1e-4):
@@ -104,6 +103,31 @@ def _grad_errors(st, sa, st64, sa64, idx):
     return np.array(e)
 
 
+def check_full_grads(case, ours, g32, g64):
+    """Full tensors (B <= 8 cases, oracle run here).  The reference's own fp32
+    step sits 1-3 % from fp64 on these B=4 steps (train-mode BN backward over
+    4x4 planes amplifies rounding; tools/step_grad_diag.py), and that error
+    varies ~10x from tensor to tensor of the same level, so a tensor's bar is
+    3x the larger of its own reference error and the 90th percentile of the
+    student's reference errors (+1e-4), and the student's median error may
+    not exceed 3.5x the reference's (measured: 0.7-3x — MFMA block sums and
+    split pieces round differently from the CPU's FMA chains, and these
+    chaotic B=4 backward passes amplify any rounding ~1e4x).  A lost loss
+    term or factor moves the median tensor by >= 10 %: the doubled-FDL case
+    mt_ubpl_fdl moves it 11.5 %."""
+    for mi, grads in ours.items():
+        rows = []
+        for n, gg in g64[mi].items():
+            if seeds.bn_cancelled(n) or float(gg.norm()) == 0:
+                continue
+            rows.append((n, float((grads[n] - gg).norm() / gg.norm()), float((g32[mi][n] - gg).norm() / gg.norm())))
+        eo, er = np.array([r[1] for r in rows]), np.array([r[2] for r in rows])
+        assert np.median(eo) <= 3.5 * np.median(er) + 1e-5, (case, mi, np.median(eo), np.median(er))
+        p90 = np.percentile(er, 90)
+        bad = [r for r in rows if r[1] > 3 * max(r[2], p90) + 1e-4]
+        assert not bad, (case, mi, p90, bad[:6])
+
+
 def check_step_grads(case, mi, rec, names, g32, g64):
     """Our gradients vs fp64, against the reference's fp32 gradients vs fp64.
     Per-parameter errors of fp32 gradients are random (one realisation per
@@ -122,9 +146,12 @@ def check_step_grads(case, mi, rec, names, g32, g64):
     for c, what in enumerate(("norm", "samples", "sum")):
         mo, mr = np.median(eo[:, c]), np.median(er[:, c])
         po, pr = np.percentile(eo[:, c], 95), np.percentile(er[:, c], 95)
-        assert mo <= 2 * mr + 1e-5, (case, mi, what, "median", mo, mr)
         assert po <= 3 * pr + 1e-4, (case, mi, what, "p95", po, pr)
-        bad = np.nonzero(eo[:, c] > 3 * er[:, c] + 10 * mr + 1e-4)[0]
+        if what == "sum":
+            continue            # a tensor's sum cancels: only its tail is compared
+        assert mo <= 2 * mr + 1e-5, (case, mi, what, "median", mo, mr)
+        # gross per-tensor errors only (the statistics of one tensor fluctuate)
+        bad = np.nonzero(eo[:, c] > 3 * er[:, c] + 10 * pr + 1e-4)[0]
         assert bad.size == 0, (case, mi, what, [(names[idx[b]], eo[b, c], er[b, c]) for b in bad[:5]])
 
 
@@ -137,22 +164,33 @@ def test_train_step_vs_reference(case, flat_adam, monkeypatch):
     g = np.load(os.path.join(GD, "steps.npz"))
     g64 = np.load(os.path.join(GD, "steps64.npz"))
     cfg = seeds.step_cases()[case]
-    ours, before, rec, counts, args, grads = _run_ours(cfg, flat_adam, monkeypatch)
+    ours, before, rec, counts, args, grads, full = _run_ours(cfg, flat_adam, monkeypatch)
     r, r32, r64 = np.array(_flat(rec, [])), g[case + "/records"], g64[case + "/records"]
     assert _noise_floor(r, r32, r64, np.abs(r64)).all(), (r, r32, r64)
     assert np.array_equal(np.array(counts, np.int64).reshape(-1, 2), g[case + "/printed_counts"])
     n_students = cfg["brNum"]
     names = [n for n, _ in ours[0].named_parameters()]
-    for mi in range(n_students):
-        check_step_grads(case, mi, grads[mi], names, g, g64)
+    if cfg["B"] > 8:
+        # B=32: the oracle's fp32/fp64 steps take minutes on a CPU; the fixtures hold
+        # the reference's and the fp64 gradient records (norm, sum, samples per tensor)
+        for mi in range(n_students):
+            check_step_grads(case, mi, grads[mi], names, g, g64)
+    else:
+        from step_oracle import oracle_grads
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        check_full_grads(case, full, oracle_grads(cfg, False), oracle_grads(cfg, True))
     for mi, (m, b0) in enumerate(zip(ours, before)):
         if mi < n_students:
-            upd = np.array([((p.detach().cpu().double() - q.cpu().double()) / args.lr).sum().item()
-                            for p, q in zip(m.parameters(), b0)])
-            ref, absu = g[case + "/model%d/upd" % mi], g[case + "/model%d/absupd" % mi]
-            noisy = np.array([seeds.bn_cancelled(n) for n in names])
-            bad = (np.abs(upd - ref) > 1e-3 * absu + 6.0) & ~noisy
-            assert not bad.any(), (mi, [names[i] for i in np.nonzero(bad)[0]][:8])
+            # AdamW's first step from the gradients checked above: p1 = p0 - lr g / (|g| + eps)
+            # (torch.optim.AdamW, step 1, weight_decay 0; bias corrections cancel)
+            for n, p, p0 in zip(names, m.parameters(), b0):
+                if n not in full[mi]:
+                    assert torch.equal(p.detach().cpu(), p0.cpu()), n       # never-trained skip_layer
+                    continue
+                gg = full[mi][n]
+                want = p0.cpu().double() - args.lr * gg / (gg.abs() + 1e-8)
+                err = (p.detach().cpu().double() - want).abs()
+                assert bool((err <= 1e-3 * args.lr + 2.5e-7 * p0.cpu().double().abs()).all()), (mi, n)
         else:
             # teacher = alpha*teacher + (1-alpha)*student_after_step (utils/parameters.py:6-8)
             for n, p, p0 in zip(names, m.parameters(), b0):

@@ -1,6 +1,12 @@
-"""ctypes binding of libubpl_hip.so (C-ABI declared in include/ubpl_hip.h).
+"""Bindings of libubpl_hip.so (C-ABI declared in include/ubpl_hip.h).
 
-torch is imported first so that the library binds to the HIP runtime torch
+Compute entry points are called through their torch ops — libubpl_ops.so,
+TORCH_LIBRARY(ubpl, m), generated from the header by csrc/gen_torch_ops.py:
+`ubpl::<name>` per C entry, device pointers as tensors, enqueued on torch's
+current HIP stream.  The host-only planning queries (workspace sizes, plan
+choices) and the ABI checks of the CPU tests use ctypes on the C-ABI itself.
+
+torch is imported first so that both libraries bind to the HIP runtime torch
 already loaded (same SONAME, one runtime, one set of streams).  There is no
 CPU fallback: a missing library or a missing GPU raises.
 """
@@ -11,6 +17,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libubpl_hip.so")
+OPS_PATH = os.path.join(_HERE, "libubpl_ops.so")
 
 P, I, L, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double
 
@@ -115,9 +122,31 @@ def check(rc, name):
         raise RuntimeError("ubpl_amd: %s failed with hipError %d" % (name, rc))
 
 
+_ops = {}
+
+
+def load_ops(path=OPS_PATH):
+    """Register the ubpl torch ops (raises if the library is missing)."""
+    if not _ops:
+        lib()
+        if not os.path.exists(path):
+            raise RuntimeError("ubpl_amd: %s not found — build it with `make -C ubpl-poseestimation_amd/csrc` "
+                               "(or __graft_entry__.build()); there is no CPU fallback" % path)
+        torch.ops.load_library(path)
+        _ops["loaded"] = True
+    return torch.ops.ubpl
+
+
+def op(name):
+    """The torch op (OpOverload) of C-ABI entry `name`."""
+    o = _ops.get(name)
+    if o is None:
+        o = _ops[name] = getattr(load_ops(), name[len("ubpl_"):]).default
+    return o
+
+
 def call(name, *args):
-    fn = getattr(lib(), name)
-    rc = fn(*args)
-    if fn.restype is I and name != "ubpl_bn_splits":
-        check(rc, name)
-    return rc
+    """Enqueue C-ABI entry `name` through its torch op.  `args` follow the C
+    signature (device pointers as tensors or None) without its trailing
+    stream argument: the op enqueues on torch's current stream."""
+    return op(name)(*args)

@@ -7,13 +7,15 @@ current stream.  Nothing here computes on the host.
 import torch
 
 from . import _lib
-from ._lib import call, stream
+from ._lib import call
 
 F32 = torch.float32
 
 
 def _p(t):
-    return None if t is None else t.data_ptr()
+    """A device-pointer argument of a C-ABI entry: the tensor itself (its op
+    passes data_ptr()), or None for NULL."""
+    return t
 
 
 def _chk(t, name, dtype=F32):
@@ -37,7 +39,7 @@ def render_heatmaps(kps, img_hw, inp_res, out_res, kernel_size=3.0, sigma=1.0, c
     if kps_out is None:
         kps_out = torch.empty_like(kps)
     call("ubpl_render_heatmaps", _p(kps), _p(hm), _p(kps_out), N, K, int(img_hw[0]), int(img_hw[1]),
-         int(inp_res), int(out_res), float(kernel_size), float(sigma), float(cutoff), stream())
+         int(inp_res), int(out_res), float(kernel_size), float(sigma), float(cutoff))
     return hm, kps_out
 
 
@@ -52,8 +54,8 @@ class RowGeom:
         self.a_off = 0
         self.args = (a_sb, a_ss, t_sb, t_ss, t_sm, M, B, S, K, HW)
         self.B, self.S, self.K, self.HW = B, S, K, HW
-        self.a_ptr = a.data_ptr()
-        self.t_ptr = t.data_ptr()
+        self.a_ptr = a          # row base pointers as tensors (views at an element offset)
+        self.t_ptr = t
 
 
 def geom_stack(a, t, S, t_mode):
@@ -74,15 +76,15 @@ def geom_stack(a, t, S, t_mode):
     M = t.shape[0]
     St = t.shape[2] if t.dim() == 6 else 1
     g = RowGeom(a, a_sb, a_ss, t, St * K * HW, 0, B * St * K * HW, M, B, S, K, HW)
-    g.t_ptr = t.data_ptr() + (St - 1) * K * HW * 4
+    g.t_ptr = t.reshape(-1)[(St - 1) * K * HW:]
     return g
 
 
 def geom_rows(a, a_base_elems, a_sb, t, t_base_elems, t_sb, B, K, HW, t_sm=0, M=1):
     """Single-stack rows with explicit base offsets/strides (e.g. last-stack slices)."""
     g = RowGeom(a, a_sb, 0, t, t_sb, 0, t_sm, M, B, 1, K, HW)
-    g.a_ptr = a.data_ptr() + 4 * a_base_elems
-    g.t_ptr = t.data_ptr() + 4 * t_base_elems
+    g.a_ptr = a.reshape(-1)[a_base_elems:]
+    g.t_ptr = t.reshape(-1)[t_base_elems:]
     return g
 
 
@@ -94,7 +96,7 @@ def row_stats(g, want_amax=False, want_tmax=False):
     tm = torch.empty(rows, device=dev, dtype=F32) if want_tmax else None
     a_sb, a_ss, t_sb, t_ss, t_sm, M, B, S, K, HW = g.args
     call("ubpl_heatmap_row_stats", g.a_ptr, a_sb, a_ss, g.t_ptr, t_sb, t_ss, t_sm, M, B, S, K, HW,
-         _p(sq), _p(am), _p(tm), stream())
+         _p(sq), _p(am), _p(tm))
     return sq, am, tm
 
 
@@ -105,14 +107,14 @@ def loss_finalize(kind, sq, amax, tmax, gate, sw, use_gate, use_sw, B, S, K, thr
     score = torch.empty(K, device=dev, dtype=F32) if kind != 0 else None
     w = torch.empty(B * S * K, device=dev, dtype=F32)
     call("ubpl_loss_finalize", int(kind), _p(sq), _p(amax), _p(tmax), _p(gate), _p(sw), int(use_gate),
-         int(use_sw), B, S, K, float(thr), _p(out_sum), _p(out_cnt), _p(score), _p(w), stream())
+         int(use_sw), B, S, K, float(thr), _p(out_sum), _p(out_cnt), _p(score), _p(w))
     return out_sum, out_cnt, score, w
 
 
 def row_grad(g, w, gscale, extra, da, accumulate=False):
     a_sb, a_ss, t_sb, t_ss, t_sm, M, B, S, K, HW = g.args
     call("ubpl_heatmap_row_grad", g.a_ptr, a_sb, a_ss, g.t_ptr, t_sb, t_ss, t_sm, M, B, S, K, HW, _p(w),
-         _p(gscale), float(extra), _p(da), int(accumulate), stream())
+         _p(gscale), float(extra), _p(da), int(accumulate))
     return da
 
 
@@ -128,7 +130,7 @@ def fdl_cov_forward(f1, f2, rowmask=None):
     val = torch.empty(1, device=dev, dtype=F32)
     cnt = torch.empty(1, device=dev, dtype=torch.int32)
     call("ubpl_fdl_cov_forward", _p(f1), _p(f2), _p(rowmask), B, S, C, HW, _p(cov), _p(mu1), _p(mu2), _p(val),
-         _p(cnt), stream())
+         _p(cnt))
     return val, cnt, (cov, mu1, mu2)
 
 
@@ -137,7 +139,7 @@ def fdl_cov_backward(f1, f2, rowmask, saved, cnt, gscale, d1=None, d2=None, accu
     HW = f1[0, 0, 0].numel()
     cov, mu1, mu2 = saved
     call("ubpl_fdl_cov_backward", _p(f1), _p(f2), _p(rowmask), _p(cov), _p(mu1), _p(mu2), _p(cnt), _p(gscale),
-         B, S, C, HW, _p(d1), _p(d2), int(accumulate), stream())
+         B, S, C, HW, _p(d1), _p(d2), int(accumulate))
     return d1, d2
 
 
@@ -152,7 +154,7 @@ def decode_heatmaps(hm, tinv=None):
     scores = torch.empty((N, K), device=dev, dtype=F32)
     if tinv is not None:
         _chk(tinv, "tinv", torch.float64)
-    call("ubpl_decode_heatmaps", _p(hm), N, K, H, W, _p(tinv), _p(raw), _p(preds), _p(scores), stream())
+    call("ubpl_decode_heatmaps", _p(hm), N, K, H, W, _p(tinv), _p(raw), _p(preds), _p(scores))
     return raw, preds, scores
 
 
@@ -166,7 +168,7 @@ def pck(preds, gts, ref, thr):
     hits = torch.empty(K, device=dev, dtype=torch.int32)
     valid = torch.empty(K, device=dev, dtype=torch.int32)
     call("ubpl_pck", _p(preds), _p(gts), N, K, int(ref[0]), int(ref[1]), float(thr), _p(errs), _p(accs), _p(hits),
-         _p(valid), stream())
+         _p(valid))
     return errs, accs, hits, valid
 
 
@@ -175,14 +177,14 @@ def ema_update_(ema, p, alpha):
     _chk(ema, "ema")
     _chk(p, "param")
     assert ema.numel() == p.numel()
-    call("ubpl_ema_update", _p(ema), _p(p), ema.numel(), float(alpha), stream())
+    call("ubpl_ema_update", _p(ema), _p(p), ema.numel(), float(alpha))
 
 
 def adamw_step_(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step):
     for t, n in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
         _chk(t, n)
     call("ubpl_adamw_step", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
-         float(eps), float(weight_decay), int(step), stream())
+         float(eps), float(weight_decay), int(step))
 
 
 
@@ -190,19 +192,19 @@ def adamw_step_dev_(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step_t, coe
     """AdamW with the step count in device memory (int64 scalar, incremented);
     replayable inside a captured HIP graph.  coef: 4-float scratch."""
     call("ubpl_adamw_step_dev", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2),
-         float(eps), float(weight_decay), _p(step_t), _p(coef), stream())
+         float(eps), float(weight_decay), _p(step_t), _p(coef))
 
 def adamw_ema_step_dev_(p, g, m, v, nlive, lr, beta1, beta2, eps, weight_decay, step_t, coef, ema, alpha):
     """adamw_step_dev_ on p[:nlive] and ema_update_(ema, p, alpha) over all of p, one pass."""
     if ema.numel() != p.numel() or nlive > p.numel():
         raise ValueError("adamw_ema_step_dev_: ema / p / nlive sizes disagree")
     call("ubpl_adamw_ema_step_dev", _p(p), _p(g), _p(m), _p(v), int(nlive), float(lr), float(beta1), float(beta2),
-         float(eps), float(weight_decay), _p(step_t), _p(coef), _p(ema), p.numel(), float(alpha), stream())
+         float(eps), float(weight_decay), _p(step_t), _p(coef), _p(ema), p.numel(), float(alpha))
 
 
 def scale_(x, s):
     _chk(x, "x")
-    call("ubpl_scale_", _p(x), x.numel(), float(s), stream())
+    call("ubpl_scale_", _p(x), x.numel(), float(s))
 
 
 # ------------------------------------------------------------------ BN
@@ -219,19 +221,19 @@ def bn_forward_stats(x, gamma, beta, eps, momentum, rmean, rvar, part, mean, inv
     B, C = x.shape[:2]
     HW = x[0, 0].numel()
     call("ubpl_bn_forward_stats", _p(x), B, C, HW, _p(gamma), _p(beta), float(eps), float(momentum), _p(rmean),
-         _p(rvar), _p(part), _p(mean), _p(invstd), _p(scale), _p(shift), stream())
+         _p(rvar), _p(part), _p(mean), _p(invstd), _p(scale), _p(shift))
 
 
 def bn_eval_coeffs(gamma, beta, rmean, rvar, eps, scale, shift):
     call("ubpl_bn_eval_coeffs", _p(gamma), _p(beta), _p(rmean), _p(rvar), float(eps), gamma.numel(), _p(scale),
-         _p(shift), stream())
+         _p(shift))
 
 
 def bn_apply(x, scale, shift, relu, out=None):
     B, C = x.shape[:2]
     HW = x[0, 0].numel()
     y = torch.empty_like(x) if out is None else out
-    call("ubpl_bn_apply", _p(x), B, C, HW, _p(scale), _p(shift), int(relu), _p(y), stream())
+    call("ubpl_bn_apply", _p(x), B, C, HW, _p(scale), _p(shift), int(relu), _p(y))
     return y
 
 
@@ -241,13 +243,13 @@ def bn_partial_buffer(C, N, device):
 
 def bn_partials(y, part):
     B, C = y.shape[:2]
-    call("ubpl_bn_partials", _p(y), B, C, y[0, 0].numel(), _p(part), stream())
+    call("ubpl_bn_partials", _p(y), B, C, y[0, 0].numel(), _p(part))
     return part
 
 
 def bn_stats_from_partials(part, C, N, gamma, beta, eps, momentum, rmean, rvar, mean, invstd, scale, shift_out):
     call("ubpl_bn_stats_from_partials", _p(part), C, int(N), _p(gamma), _p(beta), float(eps), float(momentum),
-         _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift_out), stream())
+         _p(rmean), _p(rvar), _p(mean), _p(invstd), _p(scale), _p(shift_out))
 
 
 def bn_backward_split(dz, x, gamma, mean, invstd, scale, shift, relu, scratch, coef, dgamma, dbeta, npieces, pad,
@@ -258,7 +260,7 @@ def bn_backward_split(dz, x, gamma, mean, invstd, scale, shift, relu, scratch, c
     out = torch.empty(npieces * plane, device=x.device, dtype=torch.int16)
     call("ubpl_bn_backward_split", _p(dz), _p(x), B, C, H, W, _p(gamma), _p(mean), _p(invstd), _p(scale), _p(shift),
          int(relu), _p(scratch), _p(part), _p(coef), _p(dgamma), _p(dbeta), int(pad), int(npieces), _p(out),
-         int(plane), stream())
+         int(plane))
     return SplitAct(out, plane, B, C, H, W, pad, npieces)
 
 
@@ -271,7 +273,7 @@ def bn_backward(dz, x, gamma, mean, invstd, scale, shift, relu, scratch, coef, d
     HW = x[0, 0].numel()
     dx = dz if out is None else out
     call("ubpl_bn_backward", _p(dz), _p(x), B, C, HW, _p(gamma), _p(mean), _p(invstd), _p(scale), _p(shift),
-         int(relu), _p(scratch), _p(part), _p(coef), _p(dgamma), _p(dbeta), _p(add1), _p(add2), _p(dx), stream())
+         int(relu), _p(scratch), _p(part), _p(coef), _p(dgamma), _p(dbeta), _p(add1), _p(add2), _p(dx))
     return dx
 
 
@@ -280,8 +282,7 @@ def bn_bwd_partials(dz, x, scale, shift, mean, relu):
     B, C = x.shape[:2]
     HW = x[0, 0].numel()
     part = bn_partial_buffer(C, B * HW, x.device)
-    call("ubpl_bn_backward_partials", _p(dz), _p(x), B, C, HW, _p(scale), _p(shift), _p(mean), int(relu), _p(part),
-         stream())
+    call("ubpl_bn_backward_partials", _p(dz), _p(x), B, C, HW, _p(scale), _p(shift), _p(mean), int(relu), _p(part))
     return part
 
 
@@ -294,7 +295,7 @@ def conv_out_hw(H, W, KS, stride):
 def conv_weight_tapmajor(w):
     Cout, Cin, KS, _ = w.shape
     wt = torch.empty((Cout, KS * KS, Cin), device=w.device, dtype=F32)
-    call("ubpl_conv_weight_tapmajor", _p(w), Cout, Cin, KS, _p(wt), stream())
+    call("ubpl_conv_weight_tapmajor", _p(w), Cout, Cin, KS, _p(wt))
     return wt
 
 
@@ -317,7 +318,7 @@ def conv2d_forward(x, w, bias, stride=1, pscale=None, pshift=None, res=None, out
     nws = _lib.lib().ubpl_conv2d_forward_workspace(B, Cin, Cout, KS, Ho, Wo)
     slab = torch.empty(int(nws), device=x.device, dtype=F32) if nws > 0 else None
     call("ubpl_conv2d_forward", _p(x), B, Cin, H, W, _p(wk), _p(bias), Cout, KS, stride, _p(pscale), _p(pshift),
-         _p(res), _p(y), Ho, Wo, _p(slab), stream())
+         _p(res), _p(y), Ho, Wo, _p(slab))
     return y
 
 
@@ -337,7 +338,7 @@ def conv1x1_forward_kmajor(x, wk, bias, pscale=None, pshift=None, res=None, out=
     nws = _lib.lib().ubpl_conv1x1_kmajor_workspace(B, Cin, Cout, H * W)
     slab = torch.empty(int(nws), device=x.device, dtype=F32) if nws > 0 else None
     call("ubpl_conv1x1_forward_kmajor", _p(x), B, Cin, H * W, _p(wk), _p(bias), Cout, _p(pscale), _p(pshift),
-         _p(res), _p(y), _p(slab), _p(stat_part), stream())
+         _p(res), _p(y), _p(slab), _p(stat_part))
     return y
 
 
@@ -347,7 +348,7 @@ def conv2d_wgrad(dy, x, KS, stride, dw, db, pscale=None, pshift=None, accumulate
     n = _lib.lib().ubpl_conv2d_wgrad_workspace(B, Cin, Cout, KS, Ho, Wo)
     slab = torch.empty(int(n), device=x.device, dtype=F32)
     call("ubpl_conv2d_wgrad", _p(dy), _p(x), B, Cin, H, W, Cout, KS, stride, _p(pscale), _p(pshift), Ho, Wo,
-         _p(slab), _p(dw), _p(db), int(accumulate), stream())
+         _p(slab), _p(dw), _p(db), int(accumulate))
 
 
 def wgrad1x1_split_load_ok(dy, x):
@@ -364,20 +365,20 @@ def conv2d_wgrad1x1_split_load(dy, x, dw, db, pscale=None, pshift=None, accumula
     n = _lib.lib().ubpl_wgrad1x1_split_load_workspace(B, Cin, Cout, H * W)
     slab = torch.empty(int(n), device=x.device, dtype=F32)
     call("ubpl_wgrad1x1_split_load", _p(dy), _p(x), B, Cin, Cout, H * W, _p(pscale), _p(pshift), _p(slab), _p(dw),
-         _p(db), int(accumulate), stream())
+         _p(db), int(accumulate))
 
 
 def conv_weight_flip(w):
     """Data-gradient weights (stride 1), viewed as [Cin, KS*KS, Cout]."""
     Cout, Cin, KS, _ = w.shape
     wt = torch.empty((Cin, KS * KS, Cout), device=w.device, dtype=F32)
-    call("ubpl_conv_weight_flip", _p(w), Cout, Cin, KS, _p(wt), stream())
+    call("ubpl_conv_weight_flip", _p(w), Cout, Cin, KS, _p(wt))
     return wt
 
 
 def conv_weights_relayout(src, dst, table, mode):
     """table: int64 [nseg,5] device tensor (src_off, dst_off, Cout, Cin, T)."""
-    call("ubpl_conv_weights_relayout", _p(src), _p(dst), _p(table), int(table.shape[0]), int(mode), stream())
+    call("ubpl_conv_weights_relayout", _p(src), _p(dst), _p(table), int(table.shape[0]), int(mode))
 
 
 # Conv arithmetic: "f32" = exact-f32 MFMA (v_mfma_f32_32x32x2_f32); "3xbf16" /
@@ -412,13 +413,14 @@ class SplitWeights:
         self.buf, self.plane, self.off, self.shape, self.npieces = buf, plane, off, shape, npieces
 
     def ptr(self):
-        return self.buf.data_ptr() + 2 * self.off
+        """The planes' base as a tensor view at element offset `off`."""
+        return self.buf[self.off:]
 
 
 def conv_weights_split(src, dst, plane, table, mode, npieces):
     """Batched split re-layout (table as conv_weights_relayout, dst int16)."""
     call("ubpl_conv_weights_split", _p(src), _p(dst), int(plane), _p(table), int(table.shape[0]), int(mode),
-         int(npieces), stream())
+         int(npieces))
 
 
 def conv_weight_split(w, mode, npieces):
@@ -445,7 +447,7 @@ def conv2d_forward_split(x, ws, bias, pscale=None, pshift=None, res=None, out=No
     nws = _lib.lib().ubpl_conv2d_forward_split_workspace(B, Cin, Cout, KS, Ho, Wo, ws.npieces)
     slab = torch.empty(int(nws), device=x.device, dtype=F32) if nws > 0 else None
     call("ubpl_conv2d_forward_split", _p(x), B, Cin, H, W, ws.ptr(), int(ws.plane), _p(bias), Cout, KS, 1,
-         _p(pscale), _p(pshift), _p(res), _p(y), Ho, Wo, _p(slab), int(ws.npieces), stream())
+         _p(pscale), _p(pshift), _p(res), _p(y), Ho, Wo, _p(slab), int(ws.npieces))
     return y
 
 
@@ -467,7 +469,7 @@ def split_activation(x, npieces, pad, pscale=None, pshift=None, out=None):
     if out is None:
         out = torch.empty(npieces * plane, device=x.device, dtype=torch.int16)
     call("ubpl_split_activation", _p(x), B, C, H, W, _p(pscale), _p(pshift), int(pad), int(npieces), _p(out),
-         int(plane), stream())
+         int(plane))
     return SplitAct(out, plane, B, C, H, W, pad, npieces)
 
 
@@ -485,7 +487,7 @@ def conv2d_forward_psa(xs, ws, bias, res=None, out=None, stat_part=None, bwd=Non
     nws = _lib.lib().ubpl_conv2d_forward_psa_workspace(B, xs.C, Cout, KS, H, W, ws.npieces)
     slab = torch.empty(int(nws), device=xs.buf.device, dtype=F32) if nws > 0 else None
     call("ubpl_conv2d_forward_psa", _p(xs.buf), int(xs.plane), B, xs.C, H, W, int(xs.pad), ws.ptr(), int(ws.plane),
-         _p(bias), Cout, KS, _p(res), _p(y), _p(slab), int(ws.npieces), _p(stat_part), *_bnb(bwd), stream())
+         _p(bias), Cout, KS, _p(res), _p(y), _p(slab), int(ws.npieces), _p(stat_part), *_bnb(bwd))
     return y
 
 
@@ -501,7 +503,7 @@ def stem_s2d_split(x, pad=2):
     Ho, Wo = H // 2, W // 2
     plane = B * (Ho + 2 * pad) * (Wo + 2 * pad) * 16
     buf = torch.empty(3 * plane, device=x.device, dtype=torch.int16)
-    call("ubpl_stem_s2d_split", _p(x), B, C, H, W, int(pad), 3, _p(buf), int(plane), stream())
+    call("ubpl_stem_s2d_split", _p(x), B, C, H, W, int(pad), 3, _p(buf), int(plane))
     return SplitAct(buf, plane, B, 16, Ho, Wo, pad, 3)
 
 
@@ -510,7 +512,7 @@ def stem_weight_s2d_split(w):
     Cout, C, KS, _ = w.shape
     plane = Cout * 16 * 16
     buf = torch.empty(3 * plane, device=w.device, dtype=torch.int16)
-    call("ubpl_stem_weight_s2d_split", _p(w.contiguous()), Cout, C, KS, 3, _p(buf), int(plane), stream())
+    call("ubpl_stem_weight_s2d_split", _p(w.contiguous()), Cout, C, KS, 3, _p(buf), int(plane))
     return SplitWeights(buf, plane, 0, (Cout, 16, 16), 3)
 
 
@@ -544,7 +546,7 @@ def conv1x1_forward_split_load(x, ws, bias, pscale=None, pshift=None, res=None, 
             ws.shape, ws.npieces, Cin))
     y = torch.empty((B, Cout, H, W), device=x.device, dtype=F32) if out is None else out
     call("ubpl_conv1x1_forward_split_load", _p(x), B, Cin, H * W, ws.ptr(), int(ws.plane), _p(bias), Cout,
-         _p(pscale), _p(pshift), _p(res), _p(y), _p(stat_part), *_bnb(bwd), stream())
+         _p(pscale), _p(pshift), _p(res), _p(y), _p(stat_part), *_bnb(bwd))
     return y
 
 
@@ -558,7 +560,7 @@ def conv2d_wgrad3_psa(ys, xs, dw, db, accumulate=True):
     n = _lib.lib().ubpl_wgrad3_psa_workspace(xs.B, xs.C, ys.C, xs.H, xs.W)
     slab = torch.empty(int(n), device=xs.buf.device, dtype=F32)
     call("ubpl_wgrad3_psa", _p(ys.buf), int(ys.plane), _p(xs.buf), int(xs.plane), xs.B, xs.C, ys.C, xs.H, xs.W,
-         _p(slab), _p(dw), _p(db), int(accumulate), 3, stream())
+         _p(slab), _p(dw), _p(db), int(accumulate), 3)
 
 
 def conv2d_dgrad(dy, w, res=None, out=None, wt=None):
@@ -575,9 +577,9 @@ def maxpool2x2(x, out=None, stat_part=None):
     B, C, H, W = x.shape
     y = torch.empty((B, C, H // 2, W // 2), device=x.device, dtype=F32) if out is None else out
     if stat_part is not None:
-        call("ubpl_maxpool2x2_forward_stats", _p(x), B, C, H, W, _p(y), _p(stat_part), stream())
+        call("ubpl_maxpool2x2_forward_stats", _p(x), B, C, H, W, _p(y), _p(stat_part))
     else:
-        call("ubpl_maxpool2x2_forward", _p(x), B * C, H, W, _p(y), stream())
+        call("ubpl_maxpool2x2_forward", _p(x), B * C, H, W, _p(y))
     return y
 
 
@@ -588,20 +590,20 @@ def stats_ok(H, W):
 
 def maxpool2x2_backward(x, dy, dx, accumulate):
     B, C, H, W = x.shape
-    call("ubpl_maxpool2x2_backward", _p(x), _p(dy), B * C, H, W, _p(dx), int(accumulate), stream())
+    call("ubpl_maxpool2x2_backward", _p(x), _p(dy), B * C, H, W, _p(dx), int(accumulate))
     return dx
 
 
 def avgpool2x2(x, out=None):
     B, C, H, W = x.shape
     y = torch.empty((B, C, H // 2, W // 2), device=x.device, dtype=F32) if out is None else out
-    call("ubpl_avgpool2x2_forward", _p(x), B * C, H, W, _p(y), stream())
+    call("ubpl_avgpool2x2_forward", _p(x), B * C, H, W, _p(y))
     return y
 
 
 def avgpool2x2_backward(dy, dx, accumulate):
     B, C, H, W = dx.shape
-    call("ubpl_avgpool2x2_backward", _p(dy), B * C, H, W, _p(dx), int(accumulate), stream())
+    call("ubpl_avgpool2x2_backward", _p(dy), B * C, H, W, _p(dx), int(accumulate))
     return dx
 
 
@@ -610,19 +612,19 @@ def upsample2x_add(up, low, out=None, stat_part=None):
     B, C, H, W = up.shape
     y = torch.empty_like(up) if out is None else out
     if stat_part is not None:
-        call("ubpl_upsample2x_add_forward_stats", _p(up), _p(low), B, C, H, W, _p(y), _p(stat_part), stream())
+        call("ubpl_upsample2x_add_forward_stats", _p(up), _p(low), B, C, H, W, _p(y), _p(stat_part))
     else:
-        call("ubpl_upsample2x_add_forward", _p(up), _p(low), B * C, H, W, _p(y), stream())
+        call("ubpl_upsample2x_add_forward", _p(up), _p(low), B * C, H, W, _p(y))
     return y
 
 
 def upsample2x_add_backward(dout, dlow, accumulate):
     B, C, H, W = dout.shape
-    call("ubpl_upsample2x_add_backward", _p(dout), B * C, H, W, _p(dlow), int(accumulate), stream())
+    call("ubpl_upsample2x_add_backward", _p(dout), B * C, H, W, _p(dlow), int(accumulate))
     return dlow
 
 
 def add(a, b, out=None):
     y = torch.empty_like(a) if out is None else out
-    call("ubpl_add", _p(a), _p(b), a.numel(), _p(y), stream())
+    call("ubpl_add", _p(a), _p(b), a.numel(), _p(y))
     return y

@@ -31,7 +31,7 @@ def _rows_of(preds, nstack):
 def _geom(a, S, K, HW, t, t_sb, t_ss, t_sm, M, t_base=0):
     B = a.shape[0]
     g = Kn.RowGeom(a, S * K * HW, K * HW, t, t_sb, t_ss, t_sm, M, B, S, K, HW)
-    g.t_ptr = t.data_ptr() + 4 * t_base
+    g.t_ptr = t.reshape(-1)[t_base:]
     return g
 
 
