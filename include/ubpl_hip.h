@@ -261,6 +261,20 @@ int ubpl_maxpool2x2_forward_stats(const float* x, int B, int C, int H, int W, fl
 int ubpl_upsample2x_add_forward_stats(const float* up, const float* low, int B, int C, int H, int W, float* out,
                                       float* part, void* stream);
 
+/* ---------------------------------------------------------------- f1 ----
+ * Two-view training augmentation (DS_mds.__getitem__, datasets/dataset_mds.py:41-201:
+ * fliplr utils/augment.py:216-227, noisy_mean :261-267, affine :86-156,
+ * image_colorNorm utils/process.py:151-160) on images resident in HBM.
+ * imgs uint8 BGR [N][H][W][3].  ubpl_image_mean_u8: out[n] = mean of image n / 255
+ * (the noisy_mean mu).  ubpl_augment_warp: view v samples image src_idx[v] at
+ * (mat[6v..6v+2] . (x,y,1), mat[6v+3..6v+5] . (x,y,1)) — flip and the inverse
+ * crop/scale/rotate transform folded by the host — bilinear, zero outside;
+ * noise[3v..3v+2] = (alpha, beta, enabled) of noisy_mean; out [V][3][Ho][Wo]
+ * float32 minus chan_mean[3]. */
+int ubpl_image_mean_u8(const uint8_t* imgs, int N, int64_t n_per_image, float* out, void* stream);
+int ubpl_augment_warp(const uint8_t* imgs, int H, int W, const int* src_idx, const float* mat, const float* noise,
+                      const float* img_mean, const float* chan_mean, int V, int Ho, int Wo, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,9 +54,10 @@ def import_reference():
     import utils.parameters as PR
     import utils.udaap.evaluation as UE
     import utils.mt.data as MD
+    import utils.udaap.transforms as UT
     import projects.tools as T
     from models.pose.hourglass import StackedHourglass
-    mods.update(L=L, P=P.ProcessUtils, E=E.EvaluationUtils, PR=PR, UE=UE, MD=MD,
+    mods.update(L=L, P=P.ProcessUtils, E=E.EvaluationUtils, PR=PR, UE=UE, MD=MD, UT=UT,
                 T=T.ProjectTools, SH=StackedHourglass)
     return mods
 
@@ -210,6 +211,18 @@ def gen_misc(R):
 
 
 # --------------------------------------------------------------------------
+# f1 augmentation geometry: keypoints through transform() (utils/udaap/transforms.py:151-158)
+# --------------------------------------------------------------------------
+def gen_augment(R):
+    out = {}
+    for cname, (center, scale, rot, pts) in seeds.augment_cases().items():
+        res = [[int(v) for v in R["UT"].transform(p, center, scale, [256, 256], rot=rot)] for p in pts]
+        out[cname + "/kps"] = np.array(res, np.int64)
+        out[cname + "/t"] = R["UT"].get_transform(center, scale, [256, 256], rot=rot)
+    np.savez_compressed(os.path.join(HERE, "augment.npz"), **out)
+
+
+# --------------------------------------------------------------------------
 # H1-H6 hourglass forward/backward
 # --------------------------------------------------------------------------
 def _param_stats(model):
@@ -345,7 +358,7 @@ def _flatten(x):
 if __name__ == "__main__":
     torch.set_num_threads(8)
     R = import_reference()
-    which = sys.argv[1:] or ["render", "losses", "decode", "misc", "hourglass", "steps"]
+    which = sys.argv[1:] or ["render", "losses", "decode", "misc", "augment", "hourglass", "steps"]
     for w in which:
         print("generating", w, flush=True)
         globals()["gen_" + w](R)

@@ -188,6 +188,21 @@ def sampler_cases():
 
 
 # --------------------------------------------------------------------------
+# f1 augmentation geometry cases (centre, scale, rotation, keypoints)
+# --------------------------------------------------------------------------
+def augment_cases():
+    rs = np.random.RandomState(31)
+    cases = {}
+    for i in range(6):
+        center = [128, 128] if i % 2 == 0 else [256 - 128, 128]
+        scale = 1.28 * float(np.clip(1 + 0.25 * rs.randn(), 0.75, 1.25))
+        rot = 0.0 if i == 0 else float(np.clip(30 * rs.randn(), -30, 30))
+        pts = rs.randint(1, 256, (9, 2)).astype(np.float32)
+        cases["a%d" % i] = (center, scale, rot, pts)
+    return cases
+
+
+# --------------------------------------------------------------------------
 # H1 hourglass cases
 # --------------------------------------------------------------------------
 def hg_cases():

@@ -165,3 +165,15 @@ def test_checkpoint_schema_and_selection_cpu(tmp_path):
     assert CK.load_checkpoint(path, ms2, es2, os2) == (7, [0.3, 0.31, 0.3], [1, 7, 1])
     assert torch.equal(ms2[1].weight, ms[1].weight) and torch.equal(es2[0].bias, es[0].bias)
     assert float(os2[0].state_dict()["state"][0]["step"]) == 1.0
+
+
+def test_augment_geometry_matches_reference_transform():
+    """f1: the keypoint map of the device augmentation is the reference's
+    transform() (utils/udaap/transforms.py:119-158), fixtures from the reference."""
+    from ubpl_amd import augment as AU
+    g = np.load(os.path.join(GD, "augment.npz"))
+    for cname, (center, scale, rot, pts) in seeds.augment_cases().items():
+        t = AU.get_transform(center, scale, [256, 256], rot=rot)
+        assert np.array_equal(t, g[cname + "/t"]), cname
+        got = np.array([AU.transform_point(p, t) for p in pts], np.int64)
+        assert np.array_equal(got, g[cname + "/kps"]), cname

@@ -1,0 +1,86 @@
+"""f2/f3 — validate() on the reference's Mouse validation split (500 real
+images, 9 keypoints, PCK@0.2 with ref keypoints [1, 2]; datasources/mouse.py:
+13-123, projects/MT_UBPL.py:355-408).
+
+The teachers' heatmaps are decoded and scored on the device (D1-D4); the same
+heatmaps go through the oracle's decoder and PCK (oracle/decode.py, pinned
+bit-exact to the reference by test_oracle_golden), and the per-batch records
+are folded with the reference's AvgCounters weights (bs per keypoint entry,
+bs*k for the mean).  Accuracies are compared bit-exact, errors to 1e-6.
+
+Needs data/mouse_100_500_0.3.npz (tools/pack_mouse.py; git-ignored, travels
+with the tree): skipped where it has not been built.
+"""
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import decode as OD
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PACK = os.path.join(ROOT, "data", "mouse_100_500_0.3.npz")
+
+
+def _teachers(K=9, S=2):
+    from ubpl_amd.hourglass import StackedHourglass
+    torch.manual_seed(1388)
+    ts = []
+    for _ in range(2):
+        t = StackedHourglass(K, S, "AvgPool")
+        for p in t.parameters():
+            p.detach_()
+        ts.append(t)
+    return ts
+
+
+@pytest.mark.skipif(not os.path.exists(PACK), reason="Mouse pack not built (tools/pack_mouse.py)")
+def test_validate_on_mouse_split_matches_oracle():
+    from ubpl_amd import mouse
+    from ubpl_amd import train as T
+    data = mouse.MouseData.from_pack(PACK)
+    semi, valid, lab, unlab, lidx, uidx, means, stds = data.getSemiData(100, 500, 0.3)
+    assert (len(semi), len(valid), len(lab), len(unlab)) == (100, 500, 30, 70)
+    assert sum(it["islabeled"] for it in semi) == 30 and all(semi[i]["islabeled"] == 0 for i in uidx)
+    assert all(abs(m - 0.49) < 0.1 for m in means)
+    dev = torch.device("cuda")
+    teachers = _teachers()
+    # move the running statistics off their init with train-mode forwards on training images
+    x_tr = mouse.to_device_images(data.images("train")[:16], means, dev)
+    with torch.no_grad():
+        for t in teachers:
+            t(x_tr)
+    batches = mouse.valid_batches(data, 32, dev)[:3]
+    args = types.SimpleNamespace(outRes=64, pck_ref=data.pck_ref, pck_thr=data.pck_thr)
+    preds_arr, accs, errs = T.validate(batches, teachers, args)
+    # the oracle on the same heatmaps
+    n = len(teachers) + 1
+    acc_c = [[OD.AvgCounter() for _ in range(10)] for _ in range(n)]
+    err_c = [[OD.AvgCounter() for _ in range(10)] for _ in range(n)]
+    want_preds = [[] for _ in range(n)]
+    for t in teachers:
+        t.eval()
+    with torch.no_grad():
+        for img, _, meta in batches:
+            bs, k = meta["kpsMap"].shape[:2]
+            pm = []
+            for t in teachers:
+                hm = t(img)[0][:, -1].float().cpu()
+                p, _ = OD.kps_from_heatmap(hm, meta["center"], meta["scale"], [64, 64])
+                pm.append(p)
+            pm.append(torch.stack(pm, -1).mean(-1))
+            for mi, p in enumerate(pm):
+                e, a = OD.acc_pck(p, meta["kpsMap"], data.pck_ref, data.pck_thr)
+                for idx in range(k + 1):
+                    acc_c[mi][idx].update(a[idx].item(), bs if idx < k else bs * k)
+                    err_c[mi][idx].update(e[idx].item(), bs if idx < k else bs * k)
+                want_preds[mi] += p.tolist()
+    for t in teachers:
+        t.train()
+    for mi in range(n):
+        assert np.array_equal(np.array(preds_arr[mi]), np.array(want_preds[mi])), mi
+        assert [c.avg for c in acc_c[mi]] == accs[mi], mi
+        np.testing.assert_allclose(errs[mi], [c.avg for c in err_c[mi]], rtol=1e-6, atol=1e-6)

@@ -80,6 +80,8 @@ SIGNATURES = {
     "ubpl_upsample2x_add_forward_stats": (I, [P, P, I, I, I, I, P, P, P]),
     "ubpl_upsample2x_add_backward": (I, [P, L, I, I, P, I, P]),
     "ubpl_add": (I, [P, P, L, P, P]),
+    "ubpl_image_mean_u8": (I, [P, I, L, P, P]),
+    "ubpl_augment_warp": (I, [P, I, I, P, P, P, P, P, I, I, I, P, P]),
 }
 
 _lib = None

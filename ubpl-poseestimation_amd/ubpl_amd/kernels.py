@@ -628,3 +628,26 @@ def add(a, b, out=None):
     y = torch.empty_like(a) if out is None else out
     call("ubpl_add", _p(a), _p(b), a.numel(), _p(y))
     return y
+
+
+# ------------------------------------------------------------------ f1
+def image_mean_u8(imgs):
+    """imgs uint8 [N,H,W,3] -> per-image mean / 255 (noisy_mean's mu), float32 [N]."""
+    _chk(imgs, "imgs", torch.uint8)
+    out = torch.empty(imgs.shape[0], device=imgs.device, dtype=F32)
+    call("ubpl_image_mean_u8", _p(imgs), imgs.shape[0], imgs[0].numel(), _p(out))
+    return out
+
+
+def augment_warp(imgs, src_idx, mat, noise, img_mean, chan_mean, out):
+    """One launch for V augmented views (see augment.hip): out [V,3,Ho,Wo]."""
+    _chk(imgs, "imgs", torch.uint8)
+    _chk(src_idx, "src_idx", torch.int32)
+    for t, n in ((mat, "mat"), (noise, "noise"), (img_mean, "img_mean"), (chan_mean, "chan_mean"), (out, "out")):
+        _chk(t, n)
+    V, _, Ho, Wo = out.shape
+    if mat.numel() != 6 * V or noise.numel() != 3 * V or src_idx.numel() != V:
+        raise ValueError("augment_warp: per-view tables do not match %d views" % V)
+    call("ubpl_augment_warp", _p(imgs), imgs.shape[1], imgs.shape[2], _p(src_idx), _p(mat), _p(noise),
+         _p(img_mean), _p(chan_mean), V, Ho, Wo, _p(out))
+    return out

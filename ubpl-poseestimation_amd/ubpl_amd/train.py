@@ -796,21 +796,31 @@ def train_supervised(trainLoader, model, optim, args):
 # ---------------------------------------------------------------------------
 def validate(validLoader, models_ema, args):
     """projects/MT_UBPL.py:355-408 -> (predsArray, accs_records, errs_records);
-    entries per teacher plus their mean (brNum + 1)."""
+    entries per teacher plus their mean (brNum + 1).
+
+    Teachers in eval mode, heatmaps decoded and scored on the device (D1-D4);
+    one device->host copy per batch.  Batches are (imgMap, heatmap or None,
+    meta) with meta center / scale / kpsMap.  Under torch.distributed every
+    rank validates its share of the batches (mouse.valid_batches: batch i on
+    rank i % world, meta['batch_index'] = i) with rank 0's teacher BatchNorm
+    statistics (broadcast first: train-mode teachers keep per-rank running
+    statistics); the per-batch (errs, accs, bs) rows are gathered and folded
+    into the AvgCounters in the single-device batch order, so the records are
+    exactly what one device computes (projects/MT_UBPL.py:393-397 weights:
+    bs per keypoint entry, bs*k for the mean entry)."""
     from .evaluation import EvaluationUtils
     from .losses import AvgCounters
     from .process import inverse_transforms
     n = len(models_ema) + 1
-    accs_c = [AvgCounters() for _ in range(n)]
-    errs_c = [AvgCounters() for _ in range(n)]
-    preds_arr = [[] for _ in range(n)]
+    D.broadcast_buffers(models_ema)
     for e in models_ema:
         e.eval()
     dev = models_ema[0].flat_params.device
+    rows = []                                    # (batch index, bs, k, host row, preds)
     with torch.no_grad():
         for bat, (imgMap, heatmap, meta) in enumerate(validLoader):
             img = imgMap.to(dev, non_blocking=True).float().contiguous()
-            bs, k = heatmap.shape[0], heatmap.shape[1]
+            bs, k = meta["kpsMap"].shape[:2]
             tinv = inverse_transforms(meta["center"], meta["scale"], [args.outRes, args.outRes]).to(dev)
             pm = []
             for e in models_ema:
@@ -818,19 +828,30 @@ def validate(validLoader, models_ema, args):
                 o = o[0] if isinstance(o, tuple) else o
                 _, p, _ = Kn.decode_heatmaps(o[:, -1].contiguous(), tinv)
                 pm.append(p)
-            pm.append(torch.stack(pm, -1).mean(-1))
+            pm.append(torch.stack(pm, -1).mean(-1))                   # :387 preds_mean
             gts = meta["kpsMap"].to(dev).float().contiguous()
             outs = [EvaluationUtils.acc_pck(p, gts, args.pck_ref, args.pck_thr) for p in pm]
             host = torch.cat([torch.cat([er, ac]) for er, ac in outs] + [p.reshape(-1) for p in pm]).cpu()
-            for mi in range(n):
-                errs = host[mi * 2 * (k + 1):mi * 2 * (k + 1) + k + 1]
-                accs = host[mi * 2 * (k + 1) + k + 1:(mi + 1) * 2 * (k + 1)]
-                for idx in range(k + 1):
-                    accs_c[mi].update(idx, accs[idx].item(), bs if idx < k else bs * k)
-                    errs_c[mi].update(idx, errs[idx].item(), bs if idx < k else bs * k)
-            base = n * 2 * (k + 1)
-            for mi in range(n):
-                preds_arr[mi] += host[base + mi * bs * k * 2:base + (mi + 1) * bs * k * 2].reshape(bs, k, 2).tolist()
+            rows.append((int(meta.get("batch_index", bat)), bs, k, host))
+    if D.is_dist():
+        import torch.distributed as dist
+        allrows = [None] * D.world()
+        dist.all_gather_object(allrows, [(bi, bs, k, h.tolist()) for bi, bs, k, h in rows])
+        rows = sorted(((bi, bs, k, torch.tensor(h)) for part in allrows for bi, bs, k, h in part),
+                      key=lambda r: r[0])
+    accs_c = [AvgCounters() for _ in range(n)]
+    errs_c = [AvgCounters() for _ in range(n)]
+    preds_arr = [[] for _ in range(n)]
+    for _, bs, k, host in rows:
+        for mi in range(n):
+            errs = host[mi * 2 * (k + 1):mi * 2 * (k + 1) + k + 1]
+            accs = host[mi * 2 * (k + 1) + k + 1:(mi + 1) * 2 * (k + 1)]
+            for idx in range(k + 1):
+                accs_c[mi].update(idx, accs[idx].item(), bs if idx < k else bs * k)
+                errs_c[mi].update(idx, errs[idx].item(), bs if idx < k else bs * k)
+        base = n * 2 * (k + 1)
+        for mi in range(n):
+            preds_arr[mi] += host[base + mi * bs * k * 2:base + (mi + 1) * bs * k * 2].reshape(bs, k, 2).tolist()
     for e in models_ema:
         e.train()
     return preds_arr, [c.avg() for c in accs_c], [c.avg() for c in errs_c]
