@@ -62,7 +62,7 @@ def test_augment_views_match_numpy_statement():
     o = out.cpu().numpy()
     for v, (m, noise, kk) in enumerate(draws):
         ref = _ref_warp(imgs[idx[v]], m.astype(np.float32).astype(np.float64), noise, float(mu[idx[v]]), means)
-        assert np.abs(o[v] - ref).max() < 2e-5, v
+        assert np.abs(o[v] - ref).max() < 1e-4, v          # float32 source coordinates in the kernel
         assert np.array_equal(kout[v].cpu().numpy(), kk)
     assert np.array_equal(kout[5].cpu().numpy()[:, 1:], np.zeros((9, 2), np.float32))
 
