@@ -243,7 +243,11 @@ def cpu_baseline(steps=1, B=32):
     t = time.time()
     OS.train_mt_ubpl(batches, models, emas, optims, args)
     dt = time.time() - t
+    cal = os.path.join(ROOT, "profiles", "r02_cpu_calibration_b32.json")
+    ratio = json.load(open(cal))["port_over_reference"] if os.path.exists(cal) else None
     return {"value": round(steps * B / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "reference_equivalent": round(steps * B / dt / ratio, 4) if ratio else None,
+            "port_over_reference": ratio,
             "sample": "oracle/step.py MT_UBPL step (same math as projects/MT_UBPL.py:157-352), 2-stack, "
                       "B=%d (half labeled), 256x256, K=16, %d timed step(s) = %.1f s, torch CPU fp32; "
                       "calibration vs the reference train(): profiles/r02_cpu_calibration_b4.json, _b32.json"
