@@ -193,6 +193,8 @@ def _sync_stats(local_sums, counts):
 # ---------------------------------------------------------------------------
 # a student's second-view backward on its teacher's stream (UBPL_SPLIT_BWD=0: one stream per student)
 _SPLIT_BWD = os.environ.get("UBPL_SPLIT_BWD", "1") != "0"
+# teachers' forwards on their own streams (UBPL_TEACHER_STREAMS=0: on their students' streams)
+_TEACHER_STREAMS = os.environ.get("UBPL_TEACHER_STREAMS", "1") != "0"
 
 
 class _ModelStreams:
@@ -221,11 +223,14 @@ class _ModelStreams:
             return None
         return _ModelStreams(M, dev)
 
+    # diagnostic: UBPL_ONE_SIDE=1 runs every network on ONE side stream (still not main)
+    _one = os.environ.get("UBPL_ONE_SIDE") == "1"
+
     def on(self, mi):
-        return torch.cuda.stream(self.side[mi])
+        return torch.cuda.stream(self.side[0 if self._one else mi])
 
     def on_teacher(self, mi):
-        return torch.cuda.stream(self.side[self.M + mi])
+        return torch.cuda.stream(self.side[0 if self._one else self.M + mi])
 
     def join(self, tensors=()):
         for s in self.side:
@@ -325,6 +330,28 @@ def _unflatten(spec, leaves):
         return {k: _unflatten(v, leaves) for k, v in spec[1]}
     vals = [_unflatten(v, leaves) for v in spec[1]]
     return tuple(vals) if kind == "tuple" else vals
+
+
+class _KeepAll:
+    """Diagnostic (UBPL_GRAPH_KEEPALL=1): keeps every tensor any torch op
+    allocates during the capture alive until the graph is released, so no
+    memory block is reused inside the captured step."""
+
+    def __enter__(self):
+        from torch.utils._python_dispatch import TorchDispatchMode
+        kept = self.kept = []
+
+        class Mode(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                out = func(*args, **(kwargs or {}))
+                kept.append(out)
+                return out
+        self.mode = Mode()
+        self.mode.__enter__()
+        return self
+
+    def __exit__(self, *a):
+        return self.mode.__exit__(*a)
 
 
 class _StepGraph:
@@ -444,8 +471,10 @@ class _StepGraph:
         sbatch = _unflatten(spec, self.static)
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        keep = _KeepAll() if os.environ.get("UBPL_GRAPH_KEEPALL") == "1" else contextlib.nullcontext()
+        with torch.cuda.graph(g), keep:
             self.out = self.core(self.models, self.emas, self.optims, self.args, *sbatch)
+        self._kept = getattr(keep, "kept", None)
         self.graph, self.key = g, key
         self.graph.replay()
         return self.out
@@ -482,7 +511,8 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
                 models[mi]._bwd_stream = None
                 oa.append(o)
                 fa.append(f)
-        with (mstreams.on_teacher(mi) if mstreams else contextlib.nullcontext()):
+        with (mstreams.on_teacher(mi) if mstreams and _TEACHER_STREAMS else
+              mstreams.on(mi) if mstreams else contextlib.nullcontext()):
             for a in range(A):
                 with torch.no_grad():
                     ea.append(models_ema[mi](imgs[a])[0])
