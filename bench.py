@@ -46,7 +46,18 @@ def make_args(B):
         outRes=64, lr=2.5e-4, wd=0.0, feature_mode="AvgPool")
 
 
-def make_batches(n, B, K, dev, seed):
+# BASELINE.json configs this bench can run (the driver runs the default, the headline)
+CONFIGS = {
+    "mt_ubpl": dict(project="MT_UBPL", S=2, K=16, B=32, res=256, desc="configs[1-2]: MT_UBPL, HG2, 256x256"),
+    "dualpose_hg4": dict(project="DualPose_UBPL", S=4, K=17, B=16, res=256,
+                         desc="configs[3]: DualPose_UBPL, dual HG4, K=17, 256x256, B=16/GPU"),
+    "mt_ubpl_hg8_384": dict(project="MT_UBPL", S=8, K=16, B=16, res=384,
+                            desc="configs[4]: MT_UBPL, HG8, 384x384 input / 96x96 heatmaps, B=16/GPU "
+                                 "(fp32-equivalent 6xbf16 convs, not the bf16 path)"),
+}
+
+
+def make_batches(n, B, K, dev, seed, res=256, dualpose=False):
     """Synthetic batches resident on the device: images
     U[0,1) minus the Mouse means, integer keypoints in [8, 248), unlabeled
     rows first and zeroed (TwoStreamBatchSampler order)."""
@@ -58,13 +69,16 @@ def make_batches(n, B, K, dev, seed):
         imgs, kps = [], []
         isl = torch.tensor([0] * (B - nlab) + [1] * nlab, dtype=torch.bool)
         for _a in range(2):
-            imgs.append((torch.rand(B, 3, 256, 256, generator=g) - means).to(dev))
+            imgs.append((torch.rand(B, 3, res, res, generator=g) - means).to(dev))
             k = torch.zeros(B, K, 3)
-            k[:, :, :2] = torch.randint(8, 248, (B, K, 2), generator=g).float()
+            k[:, :, :2] = torch.randint(8, res - 8, (B, K, 2), generator=g).float()
             k[:, :, 2] = 1.0
             k[~isl] = 0.0
             kps.append(k.to(dev))
-        out.append((imgs, None, {"kps": kps, "islabeled": [isl.to(dev)]}))
+        if dualpose:       # (stu_img, stu_heatmap, ema_img, meta): DualPose_UBPL.py:171
+            out.append((imgs[0], None, imgs[1], {"kps": kps[0], "islabeled": isl.to(dev)}))
+        else:
+            out.append((imgs, None, {"kps": kps, "islabeled": [isl.to(dev)]}))
     return out
 
 
@@ -259,9 +273,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--config", default="mt_ubpl", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
+    cfg = CONFIGS[a.config]
+    headline = a.config == "mt_ubpl"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -280,12 +297,14 @@ def main():
     from ubpl_amd import dist as D
     _lib.load()
 
-    B, K = a.batch, 16
+    B, K, S, res = a.batch or cfg["B"], cfg["K"], cfg["S"], cfg["res"]
+    dualpose = cfg["project"] == "DualPose_UBPL"
+    train = T.train_dualpose_ubpl if dualpose else T.train_mt_ubpl
     torch.manual_seed(1388)
     models, emas, optims = [], [], []
     for _ in range(2):                               # projects/MT_UBPL.py:43-50
-        m = StackedHourglass(K, 2, "AvgPool")
-        e = StackedHourglass(K, 2, "AvgPool")
+        m = StackedHourglass(K, S, "AvgPool")
+        e = StackedHourglass(K, S, "AvgPool")
         for p in e.parameters():
             p.detach_()
         models.append(m)
@@ -293,7 +312,8 @@ def main():
         optims.append(FlatAdamW(m, lr=2.5e-4, weight_decay=0.0))
     D.broadcast_params(models + emas)
     args = make_args(B)
-    batches = make_batches(2, B, K, dev, 1388 + rank)
+    args.nStack, args.outRes = S, res // 4
+    batches = make_batches(2, B, K, dev, 1388 + rank, res, dualpose)
     warm = [batches[i % 2] for i in range(a.warmup)]
     timed = [batches[i % 2] for i in range(a.steps)]
 
@@ -302,13 +322,13 @@ def main():
     # UBPL_STEP_GRAPH=1 forces it — then it is captured on the last warm-up
     # step and the timed steps are replays)
     T._StepGraph.WARM = max(1, a.warmup - 1)
-    T.train_mt_ubpl(warm, models, emas, optims, args, verbose=False)
+    train(warm, models, emas, optims, args, verbose=False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    T.train_mt_ubpl(timed, models, emas, optims, args, verbose=False)
+    train(timed, models, emas, optims, args, verbose=False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -317,7 +337,7 @@ def main():
     # roofline kernel: its launches from one more (eager, untimed) step, replayed
     # back to back between HIP events (standalone duration; see roofline())
     args.batch = B
-    roof = roofline(Kn, _lib, T, models, emas, optims, args, timed[0], dt / a.steps * 1e3)
+    roof = roofline(Kn, _lib, T, models, emas, optims, args, timed[0], dt / a.steps * 1e3) if headline else None
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -325,19 +345,22 @@ def main():
     images = world * B * a.steps
     if rank == 0:
         cpu = None
-        if not a.no_cpu_baseline and world == 1:
+        if not a.no_cpu_baseline and world == 1 and headline:
             cpu = cpu_baseline()
         line = {
-            "metric": METRIC, "value": round(images / dt, 3), "unit": "images/sec", "n_gpus": world,
+            "metric": METRIC if headline else "images/sec training step (%s)" % cfg["desc"],
+            "value": round(images / dt, 3), "unit": "images/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "conv_precision": Kn.conv_precision_name(),
             "data": "synthetic (U[0,1) images - means, integer keypoints, half labeled; heatmaps rendered on device)",
-            "config": {"workload": "MT_UBPL train step, 2 students + 2 EMA teachers, 2 views",
-                       "model": "StackedHourglass HG2 (K=16, AvgPool features)", "global_batch": B * world,
-                       "per_gpu_batch": B, "input": "256x256x3", "heatmap": "16x64x64",
-                       "parallelism": "dp%d" % world},
-            "roofline": roof, "cpu_baseline": cpu, "pck": pck_record(),
+            "config": {"workload": ("%s train step, 2 students + 2 EMA teachers, %s" % (
+                                        cfg["project"], "student / teacher views" if dualpose else "2 views")),
+                       "model": "StackedHourglass HG%d (K=%d, AvgPool features)" % (S, K), "global_batch": B * world,
+                       "per_gpu_batch": B, "input": "%dx%dx3" % (res, res),
+                       "heatmap": "%dx%dx%d" % (K, res // 4, res // 4), "parallelism": "dp%d" % world,
+                       "baseline_config": cfg["desc"]},
+            "roofline": roof, "cpu_baseline": cpu, "pck": pck_record() if headline else None,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
