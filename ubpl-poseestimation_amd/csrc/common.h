@@ -86,23 +86,31 @@ inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // res may alias the output.  The cases are wave-uniform branches; inside one,
 // loads are unconditional (clamped rows): a load under a per-lane condition
 // becomes a branch + vmcnt(0) per element.  No residual: nothing is read.
-template <int TM, int TN, typename ACC>
+// GROUPED: a scheduling barrier after each fragment's 16 loads (their
+// addresses die once issued) — keeps the widest tiles (conv_psa 128 x 256)
+// within 256 VGPRs without scratch.
+template <int TM, int TN, bool GROUPED = false, typename ACC>
 __device__ __forceinline__ void seed_acc(ACC (&acc)[TM][TN], const float* bias, const float* res,
                                          const int64_t (&obase)[TN], int mrow0, int M, int P) {
     const int h = (threadIdx.x & 63) >> 5;
     if (res != nullptr) {
         const bool hb = bias != nullptr;
         const float* bp = hb ? bias : res;
+        // 32-bit offsets from one base per fragment column: with a 64-bit
+        // address per element live at once the wide kernels spilled to scratch
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i) {
+                const float* rj = res + obase[j];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = min(mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
                     const float bv = bp[m];
-                    acc[i][j][r] = (hb ? bv : 0.f) + res[obase[j] + (int64_t)m * P];
+                    acc[i][j][r] = (hb ? bv : 0.f) + rj[m * P];
                 }
+                if (GROUPED) __builtin_amdgcn_sched_barrier(0);
+            }
     } else if (bias != nullptr) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)

@@ -401,7 +401,10 @@ __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int KS, int NP, int BNT = 128, int WGM = 2>
+// EPI: the opt-in BatchNorm-partials epilogues (UBPL_FWD_EPI / UBPL_BWD_EPI)
+// are compiled in; without them the kernel needs no scratch (the epilogue's
+// register pressure spilled ~190 VGPRs to scratch in every launch).
+template <int BM, int KS, int NP, int BNT = 128, int WGM = 2, bool EPI = false>
 __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
@@ -488,7 +491,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
     }
     floatx16 acc[TM][TN];
     const bool direct = slab == nullptr;
-    ubpl::seed_acc<TM, TN>(acc, direct ? bias : nullptr, direct ? res : nullptr, obase, m0 + wm, Cout, P);
+    ubpl::seed_acc<TM, TN, true>(acc, direct ? bias : nullptr, direct ? res : nullptr, obase, m0 + wm, Cout, P);
 
     const int nkt = (k_end - k_begin) >> 4;
     if (nkt > 0) stage(0, k_begin);
@@ -573,8 +576,8 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
         }
         return;
     }
-    if (stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0 + wm, Cout, n0 + wn, N, stat_part);
-    if (bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, n0 + wn, N, bwd);
+    if (EPI && stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0 + wm, Cout, n0 + wn, N, stat_part);
+    if (EPI && bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, n0 + wn, N, bwd);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         if (!nok[j]) continue;
@@ -601,7 +604,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 // planes of [M][K] (ubpl_conv_weights_split with KS = 1), staged as in
 // conv_psa_kernel.  2-stage ring, 2 workgroups per CU.  The activation read is
 // the f32 tensor itself: no split pass, no 6-byte/element PSA image.
-template <int BM, bool PRO>
+template <int BM, bool PRO, bool EPI = false>
 __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restrict__ x,
                                                            const uint16_t* __restrict__ wp, int64_t wplane,
                                                            const float* __restrict__ bias,
@@ -735,8 +738,8 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 
-    if (stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0, M, n0 + wn, N, stat_part);
-    if (bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0, M, P, n0 + wn, N, bwd);
+    if (EPI && stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0, M, n0 + wn, N, stat_part);
+    if (EPI && bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0, M, P, n0 + wn, N, bwd);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         if (!nok[j]) continue;
@@ -1399,9 +1402,13 @@ int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t w
     dim3 grid((unsigned)((N + BNT - 1) / BNT), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
     const bool split = pl.splits > 1;
     const ubpl::BnBwdEpi off{nullptr, nullptr, 0, nullptr};
-    hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM>), grid, dim3(NT), 0, st, xs, xplane, wp, wplane, bias,
-                       split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr,
-                       split ? nullptr : stat_part, split ? off : bwd);
+    if (!split && (stat_part || bwd.part))
+        hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM, true>), grid, dim3(NT), 0, st, xs, xplane, wp,
+                           wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl.kchunk, nullptr, stat_part, bwd);
+    else
+        hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM>), grid, dim3(NT), 0, st, xs, xplane, wp, wplane,
+                           bias, split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr,
+                           nullptr, off);
     UBPL_LAUNCH_CHECK();
     if (split) {
         launch_split_reduce(slab, pl.splits, Cout, H * W, N, bias, res, y, st);
@@ -1540,7 +1547,7 @@ UBPL_API int ubpl_conv_weights_split(const float* src, uint16_t* dst, int64_t pl
 UBPL_API int ubpl_split_activation(const float* x, int B, int C, int H, int W, const float* pscale,
                                    const float* pshift, int pad, int npieces, uint16_t* dst, int64_t plane,
                                    void* stream) {
-    if (C % 16 != 0 || npieces < 2 || npieces > 3 || pad < 0 || (plane % 8) != 0) return (int)hipErrorInvalidValue;
+    if (C % 16 != 0 || npieces < 1 || npieces > 3 || pad < 0 || (plane % 8) != 0) return (int)hipErrorInvalidValue;
     const int Hp = H + 2 * pad, Wp = W + 2 * pad;
     dim3 grid((unsigned)((Hp * Wp + 255) / 256), (unsigned)(C / 16), (unsigned)B);
     hipStream_t st = (hipStream_t)stream;
@@ -1548,7 +1555,10 @@ UBPL_API int ubpl_split_activation(const float* x, int B, int C, int H, int W, c
 #define UBPL_SA(NP_, PRO_)                                                                                      \
     hipLaunchKernelGGL((split_act_kernel<NP_, PRO_>), grid, dim3(256), 0, st, x, C, H, W, pscale, pshift, pad, \
                        dst, plane)
-    if (npieces == 2) {
+    if (npieces == 1) {   // the "bf16" precision: one piece = bf16(v)
+        if (pro) UBPL_SA(1, true);
+        else UBPL_SA(1, false);
+    } else if (npieces == 2) {
         if (pro) UBPL_SA(2, true);
         else UBPL_SA(2, false);
     } else {
@@ -1575,7 +1585,7 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
                                      const float* bn_x, const float* bn_coef, int bn_relu, float* bn_part,
                                      void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    if (Cin % 16 != 0 || (npieces != 2 && npieces != 3) || pad < KS / 2 || (KS != 1 && KS != 3 && KS != 4))
+    if (Cin % 16 != 0 || npieces < 1 || npieces > 3 || pad < KS / 2 || (KS != 1 && KS != 3 && KS != 4))
         return (int)hipErrorInvalidValue;
     const ubpl::BnBwdEpi bwd{bn_part ? bn_x : nullptr, bn_coef, bn_relu, bn_part};
     if ((((uintptr_t)wsplit) & 15) != 0 || (((uintptr_t)xs) & 15) != 0 || (wplane % 8) != 0 || (xplane % 8) != 0)
@@ -1601,10 +1611,24 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         return launch_psa<64, 4, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                             slab, stat_part, bwd, st);
     }
-    if (bm64w && pl.bm == 64 && pl.splits == 1 && npieces == 3 && KS == 3 && N % 256 == 0)
-        return launch_psa<64, 3, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
+    if (bm64w && pl.bm == 64 && pl.splits == 1 && npieces != 2 && N % 256 == 0 && (KS == 3 || npieces == 1)) {
+        if (npieces == 3)
+            return launch_psa<64, 3, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
+                                                slab, stat_part, bwd, st);
+        if (KS == 3)
+            return launch_psa<64, 3, 1, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
+                                                slab, stat_part, bwd, st);
+        return launch_psa<64, 1, 1, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                             slab, stat_part, bwd, st);
-    if (bn256 && pl.bm == 128 && pl.splits == 1 && npieces == 3 && N % 256 == 0) {
+    }
+    if (bn256 && pl.bm == 128 && pl.splits == 1 && npieces != 2 && N % 256 == 0) {
+        if (npieces == 1) {
+            if (KS == 3)
+                return launch_psa<128, 3, 1, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout,
+                                                  pl, slab, stat_part, bwd, st);
+            return launch_psa<128, 1, 1, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
+                                              slab, stat_part, bwd, st);
+        }
         if (KS == 3)
             return launch_psa<128, 3, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                               slab, stat_part, bwd, st);
@@ -1618,10 +1642,12 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     if (pl.bm == 128) UBPL_PS(128, KS_, NP_); \
     UBPL_PS(64, KS_, NP_)
     if (KS == 1) {
+        if (npieces == 1) { UBPL_PS_BM(1, 1); }
         if (npieces == 2) { UBPL_PS_BM(1, 2); }
         UBPL_PS_BM(1, 3);
     }
     if (KS == 3) {
+        if (npieces == 1) { UBPL_PS_BM(3, 1); }
         if (npieces == 2) { UBPL_PS_BM(3, 2); }
         UBPL_PS_BM(3, 3);
     }
@@ -1666,9 +1692,16 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     const int bm = Cout % 128 == 0 ? 128 : 64;
     const ubpl::BnBwdEpi bwd{bn_part ? bn_x : nullptr, bn_coef, bn_relu, bn_part};
     dim3 grid((unsigned)((N + 255) / 256), (unsigned)(Cout / bm));
+    const bool epi = stat_part != nullptr || bn_part != nullptr;
 #define UBPL_SOL(BM_, PRO_)                                                                                       \
-    hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_>), grid, dim3(NT), 0, st, x, wsplit, wplane, bias, pscale, \
-                       pshift, res, y, B, Cin, P, Cout, stat_part, bwd)
+    do {                                                                                                          \
+        if (epi)                                                                                                  \
+            hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, true>), grid, dim3(NT), 0, st, x, wsplit, wplane,   \
+                               bias, pscale, pshift, res, y, B, Cin, P, Cout, stat_part, bwd);                    \
+        else                                                                                                      \
+            hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_>), grid, dim3(NT), 0, st, x, wsplit, wplane, bias,   \
+                               pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);                            \
+    } while (0)
     if (bm == 128) {
         if (pro) UBPL_SOL(128, true);
         else UBPL_SOL(128, false);
@@ -1712,7 +1745,8 @@ UBPL_API int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t
                              int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,
                              void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    if (Cin % 64 || Cout % 64 || W % 16 || npieces != 3 || slab == nullptr) return (int)hipErrorInvalidValue;
+    if (Cin % 64 || Cout % 64 || W % 16 || (npieces != 3 && npieces != 1) || slab == nullptr)
+        return (int)hipErrorInvalidValue;
     if ((((uintptr_t)dys) & 15) || (((uintptr_t)xs) & 15) || (dplane % 8) || (xplane % 8)) return (int)hipErrorInvalidValue;
     const int splits = wgrad3_splits(B, Cin, Cout, H, W);
     const int steps = B * H * (W / 16);
@@ -1720,12 +1754,20 @@ UBPL_API int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t
     const int cb = wgrad3_cb(Cin, Cout);
     if (cb == 128) {
         dim3 grid((unsigned)(9 * (Cin / cb)), (unsigned)(Cout / cb), (unsigned)splits);
-        hipLaunchKernelGGL((wgrad3_psa_kernel<3, 128>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout,
-                           H, W, per, slab);
+        if (npieces == 1)
+            hipLaunchKernelGGL((wgrad3_psa_kernel<1, 128>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin,
+                               Cout, H, W, per, slab);
+        else
+            hipLaunchKernelGGL((wgrad3_psa_kernel<3, 128>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin,
+                               Cout, H, W, per, slab);
     } else {
         dim3 grid((unsigned)(3 * (Cin / 64)), (unsigned)(Cout / 64), (unsigned)splits);
-        hipLaunchKernelGGL((wgrad3_psa64_kernel<3>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout, H,
-                           W, per, slab);
+        if (npieces == 1)
+            hipLaunchKernelGGL((wgrad3_psa64_kernel<1>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout,
+                               H, W, per, slab);
+        else
+            hipLaunchKernelGGL((wgrad3_psa64_kernel<3>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout,
+                               H, W, per, slab);
     }
     UBPL_LAUNCH_CHECK();
     return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 9, db != nullptr, dw, db, accumulate, stream);

@@ -4,6 +4,8 @@ Each wrapper validates device / dtype / contiguity, allocates outputs with
 the torch caching allocator on the input's device and enqueues on torch's
 current stream.  Nothing here computes on the host.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -383,8 +385,10 @@ def conv_weights_relayout(src, dst, table, mode):
 
 # Conv arithmetic: "f32" = exact-f32 MFMA (v_mfma_f32_32x32x2_f32); "3xbf16" /
 # "6xbf16" = split-bf16 MFMA with 2 / 3 bf16 pieces per f32 operand (3 / 6
-# piece products, f32 accumulation).  Value = pieces (0 for f32).
-CONV_PRECISIONS = {"f32": 0, "3xbf16": 2, "6xbf16": 3}
+# piece products, f32 accumulation); "bf16" = one piece, i.e. both operands
+# rounded to bf16 (RNE) with f32 accumulation — the throughput precision of
+# BASELINE config 5 (8 stacks, 384x384), not parity-grade.  Value = pieces (0 for f32).
+CONV_PRECISIONS = {"f32": 0, "bf16": 1, "3xbf16": 2, "6xbf16": 3}
 DEFAULT_CONV_PRECISION = "6xbf16"
 
 
@@ -516,10 +520,13 @@ def stem_weight_s2d_split(w):
     return SplitWeights(buf, plane, 0, (Cout, 16, 16), 3)
 
 
+_NO_SOL = os.environ.get("UBPL_NO_SOL") == "1"      # diagnostic: every 1x1 on the exact-f32 kernels
+
+
 def conv1x1_split_load_ok(x, ws):
     """The 6xbf16 split-on-load 1x1 kernel takes this shape and fills the chip."""
     B, Cin, H, W = x.shape
-    return (ws is not None and ws.npieces == 3 and ws.shape[1] == 1 and ws.shape[2] == Cin
+    return (not _NO_SOL and ws is not None and ws.npieces == 3 and ws.shape[1] == 1 and ws.shape[2] == Cin
             and x.data_ptr() % 16 == 0
             and bool(_lib.lib().ubpl_conv1x1_split_load_preferred(B, Cin, ws.shape[0], H * W)))
 
@@ -551,7 +558,7 @@ def conv1x1_forward_split_load(x, ws, bias, pscale=None, pshift=None, res=None, 
 
 
 def wgrad3_psa_ok(ys, xs):
-    return (ys.npieces == 3 and xs.npieces == 3 and ys.pad == 1 and xs.pad == 1 and xs.C % 64 == 0
+    return (ys.npieces in (1, 3) and xs.npieces == ys.npieces and ys.pad == 1 and xs.pad == 1 and xs.C % 64 == 0
             and ys.C % 64 == 0 and xs.W % 16 == 0 and (ys.B, ys.H, ys.W) == (xs.B, xs.H, xs.W))
 
 
@@ -560,7 +567,7 @@ def conv2d_wgrad3_psa(ys, xs, dw, db, accumulate=True):
     n = _lib.lib().ubpl_wgrad3_psa_workspace(xs.B, xs.C, ys.C, xs.H, xs.W)
     slab = torch.empty(int(n), device=xs.buf.device, dtype=F32)
     call("ubpl_wgrad3_psa", _p(ys.buf), int(ys.plane), _p(xs.buf), int(xs.plane), xs.B, xs.C, ys.C, xs.H, xs.W,
-         _p(slab), _p(dw), _p(db), int(accumulate), 3)
+         _p(slab), _p(dw), _p(db), int(accumulate), int(xs.npieces))
 
 
 def conv2d_dgrad(dy, w, res=None, out=None, wt=None):
