@@ -54,6 +54,9 @@ CONFIGS = {
     "mt_ubpl_hg8_384": dict(project="MT_UBPL", S=8, K=16, B=16, res=384,
                             desc="configs[4]: MT_UBPL, HG8, 384x384 input / 96x96 heatmaps, B=16/GPU "
                                  "(fp32-equivalent 6xbf16 convs, not the bf16 path)"),
+    "mt_ubpl_hg8_384_bf16": dict(project="MT_UBPL", S=8, K=16, B=16, res=384, precision="bf16",
+                                 desc="configs[4]: MT_UBPL, HG8, 384x384 input / 96x96 heatmaps, B=16/GPU, "
+                                      "bf16 MFMA path (conv operands bf16, f32 accumulation)"),
 }
 
 
@@ -279,6 +282,8 @@ def main():
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
     headline = a.config == "mt_ubpl"
+    if "precision" in cfg:
+        os.environ["UBPL_CONV_PRECISION"] = cfg["precision"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -351,7 +356,8 @@ def main():
             "metric": METRIC if headline else "images/sec training step (%s)" % cfg["desc"],
             "value": round(images / dt, 3), "unit": "images/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if Kn.conv_precision_name() == "bf16" else "fp32",
             "conv_precision": Kn.conv_precision_name(),
             "data": "synthetic (U[0,1) images - means, integer keypoints, half labeled; heatmaps rendered on device)",
             "config": {"workload": ("%s train step, 2 students + 2 EMA teachers, %s" % (

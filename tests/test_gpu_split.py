@@ -144,6 +144,69 @@ def test_psa_forward_and_dgrad_vs_f64(case, npieces):
     assert esp <= 2 * e32 + 1e-8, (esp, e32)
 
 
+@pytest.mark.parametrize("case", CASES)
+def test_bf16_psa_forward_and_dgrad_vs_rounded_f64(case):
+    """The "bf16" precision (one piece per operand): the PSA kernels with NP = 1
+    compute the conv of the bf16-rounded (RNE) operands with f32 accumulation —
+    against float64 on exactly those rounded operands, to f32 summation error."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, H, Cout, KS, pro, resid = case
+    gen = torch.Generator().manual_seed(29 + hash(case) % 1000)
+    x32 = torch.randn(B, Cin, H, H, generator=gen)
+    w32 = torch.randn(Cout, Cin, KS, KS, generator=gen) / np.sqrt(Cin * KS * KS)
+    b32 = torch.randn(Cout, generator=gen)
+    sc32 = torch.rand(Cin, generator=gen) + 0.5
+    sh32 = torch.randn(Cin, generator=gen) * 0.5
+    res32 = torch.randn(B, Cout, H, H, generator=gen) if resid else None
+    bf = lambda t: t.to(torch.bfloat16).double()
+    inp = F.relu((x32.double() * sc32.double()[None, :, None, None] + sh32.double()[None, :, None, None]).float()) \
+        if pro else x32
+    yref = F.conv2d(bf(inp), bf(w32), b32.double(), 1, (KS - 1) // 2)
+    if resid:
+        yref = yref + res32.double()
+    d = lambda t: None if t is None else t.to(DEV)
+    ps, ph = (d(sc32), d(sh32)) if pro else (None, None)
+    for pad in sorted({(KS - 1) // 2, 1}):
+        xs = Kn.split_activation(d(x32), 1, pad, ps, ph)
+        ws = Kn.conv_weight_split(d(w32), 0, 1)
+        y = Kn.conv2d_forward_psa(xs, ws, d(b32), res=d(res32))
+        e = _rel(y, yref)
+        print("bf16 psa fwd %s pad=%d: %.2e" % (case, pad, e))
+        assert e <= 2e-6, (pad, e)
+    dy = torch.randn(B, Cout, H, H, generator=gen)
+    dxref = torch.nn.grad.conv2d_input((B, Cin, H, H), bf(w32), bf(dy), 1, (KS - 1) // 2)
+    ys = Kn.split_activation(d(dy), 1, (KS - 1) // 2)
+    wd = Kn.conv_weight_split(d(w32), 1, 1)
+    e = _rel(Kn.conv2d_forward_psa(ys, wd, None), dxref)
+    print("bf16 psa dgrad %s: %.2e" % (case, e))
+    assert e <= 2e-6, e
+
+
+@pytest.mark.parametrize("case", [(2, 128, 128, 64, 64), (2, 64, 64, 32, 32), (3, 128, 64, 16, 32)])
+def test_bf16_wgrad3_psa_vs_rounded_f64(case):
+    """3x3 weight gradient with NP = 1 operands vs float64 of the bf16-rounded operands."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, Cout, H, W = case
+    gen = torch.Generator().manual_seed(43 + hash(case) % 1000)
+    x = torch.randn(B, Cin, H, W, generator=gen)
+    dy = torch.randn(B, Cout, H, W, generator=gen)
+    sc, sh = torch.rand(Cin, generator=gen) + 0.5, torch.randn(Cin, generator=gen) * 0.5
+    bf = lambda t: t.to(torch.bfloat16).double()
+    inp = F.relu((x.double() * sc.double()[None, :, None, None] + sh.double()[None, :, None, None]).float())
+    dwref = torch.nn.grad.conv2d_weight(bf(inp), (Cout, Cin, 3, 3), bf(dy), 1, 1)
+    dbref = bf(dy).sum((0, 2, 3))
+    d = lambda t: t.to(DEV)
+    xs = Kn.split_activation(d(x), 1, 1, d(sc), d(sh))
+    ys = Kn.split_activation(d(dy), 1, 1)
+    assert Kn.wgrad3_psa_ok(ys, xs)
+    dw, db = torch.zeros(Cout, Cin, 3, 3, device=DEV), torch.zeros(Cout, device=DEV)
+    Kn.conv2d_wgrad3_psa(ys, xs, dw, db, accumulate=False)
+    e = _rel(dw, dwref)
+    print("bf16 wgrad3 %s: %.2e" % (case, e))
+    assert e <= 2e-6, e
+    assert _rel(db, dbref) <= 1e-5
+
+
 def test_split_activation_layout():
     """PSA image: pieces sum back to relu(x*s+h) exactly, border zero, [B][C/16][Hp][Wp][16]."""
     from ubpl_amd import kernels as Kn
@@ -204,18 +267,20 @@ def test_bn_backward_split_matches_f32_then_split():
     sc, sh = gamma * istd, d(torch.randn(C, generator=gen)) - mean * gamma * istd
     part = torch.zeros(int(__import__("ubpl_amd")._lib.lib().ubpl_bn_part_doubles(B, C)), dtype=torch.float64,
                        device=DEV)
-    outs = []
-    for mode in ("f32", "split"):
-        coef = torch.empty(3 * C, device=DEV)
-        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
-        if mode == "f32":
-            dx = Kn.bn_backward(dz, x, gamma, mean, istd, sc, sh, 1, part, coef, dg, db, out=torch.empty_like(dz))
-            ys = Kn.split_activation(dx, 3, 1)
-        else:
-            ys = Kn.bn_backward_split(dz, x, gamma, mean, istd, sc, sh, 1, part, coef, dg, db, 3, 1)
-        outs.append((ys.buf.cpu(), dg.cpu(), db.cpu()))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for npieces in (3, 1):
+        outs = []
+        for mode in ("f32", "split"):
+            coef = torch.empty(3 * C, device=DEV)
+            dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+            if mode == "f32":
+                dx = Kn.bn_backward(dz, x, gamma, mean, istd, sc, sh, 1, part, coef, dg, db,
+                                    out=torch.empty_like(dz))
+                ys = Kn.split_activation(dx, npieces, 1)
+            else:
+                ys = Kn.bn_backward_split(dz, x, gamma, mean, istd, sc, sh, 1, part, coef, dg, db, npieces, 1)
+            outs.append((ys.buf.cpu(), dg.cpu(), db.cpu()))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), npieces
 
 
 # (B, Cin, H, Cout, prologue, residual): 128- and 64-row tiles, a pixel tail

@@ -697,7 +697,7 @@ UBPL_API int ubpl_bn_backward_split(const float* dz, const float* x, int B, int 
                                     int relu, double* scratch, const float* part, float* coef, float* dgamma,
                                     float* dbeta, int pad, int npieces, uint16_t* dst, int64_t plane, void* stream) {
     const int HW = H * W;
-    if (C % 16 != 0 || npieces < 2 || npieces > 3 || pad < 0) return (int)hipErrorInvalidValue;
+    if (C % 16 != 0 || npieces < 1 || npieces > 3 || pad < 0) return (int)hipErrorInvalidValue;
     hipStream_t st = (hipStream_t)stream;
     const int e = bwd_stats(dz, x, B, C, HW, gamma, mean, invstd, scale, shift, relu, scratch, part, coef, dgamma,
                             dbeta, st);
@@ -707,6 +707,9 @@ UBPL_API int ubpl_bn_backward_split(const float* dz, const float* x, int B, int 
     dim3 grid((unsigned)((Hp * Wp + 255) / 256), (unsigned)(C / 16), (unsigned)B);
     if (npieces == 3)
         hipLaunchKernelGGL(bwd_apply_split_kernel<3>, grid, dim3(256), 0, st, dz, x, C, H, W, scale, shift, mean,
+                           relu, ca, cb, cc, pad, dst, plane);
+    else if (npieces == 1)
+        hipLaunchKernelGGL(bwd_apply_split_kernel<1>, grid, dim3(256), 0, st, dz, x, C, H, W, scale, shift, mean,
                            relu, ca, cb, cc, pad, dst, plane);
     else
         hipLaunchKernelGGL(bwd_apply_split_kernel<2>, grid, dim3(256), 0, st, dz, x, C, H, W, scale, shift, mean,

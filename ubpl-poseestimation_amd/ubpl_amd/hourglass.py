@@ -244,8 +244,12 @@ class StackedHourglass(nn.Module):
                  planes fill the chip on the same arithmetic with the activations
                  split while they are staged, the rest f32;
         '3xbf16' every conv with 16-channel contraction groups on the 2-piece
-                 register-staged split kernel (faster, ~2^-16 operands: not parity-grade).
-        The stem (7x7, stride 2, 3 input channels) always runs in f32."""
+                 register-staged split kernel (faster, ~2^-16 operands: not parity-grade);
+        'bf16'   every conv with 16-channel contraction groups (3x3 and 1x1, all three
+                 directions) on the PSA kernels with ONE piece per operand = bf16
+                 operands, f32 accumulation (BASELINE config 5's throughput path).
+        The stem (7x7, stride 2, 3 input channels) runs in f32 except on the
+        6xbf16 space-to-depth path."""
         self.conv_pieces = Kn.conv_precision_pieces(name)
         self._build_weight_tables()
 
@@ -575,9 +579,9 @@ class _Exec:
                 return Kn.conv1x1_forward_split_load(x, ws, b, ps, ph, res=res, out=out, stat_part=part), part
             ws = None                                    # small plane: the f32 1x1 kernel
         if ws is not None:
-            if ws.npieces == 3:
+            if ws.npieces in (1, 3):
                 part = mkpart()
-                xs = Kn.split_activation(x, 3, (ws.shape[1] == 9) * 1, ps, ph)
+                xs = Kn.split_activation(x, ws.npieces, (ws.shape[1] == 9) * 1, ps, ph)
                 if self.do_save and ws.shape[1] == 9:
                     self.saved_split[name] = xs          # the 3x3 weight gradient's B operand
                 return Kn.conv2d_forward_psa(xs, ws, b, res=res, out=out, stat_part=part), part
@@ -660,8 +664,8 @@ class _Exec:
     def bn_bwd_split(self, name, dz, x, relu, part=None):
         sc, sh, mu, istd = self.bnc(name)
         return Kn.bn_backward_split(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.bpart,
-                                    self._coef(), self.G(name + ".weight"), self.G(name + ".bias"), 3, 1,
-                                    part=part)
+                                    self._coef(), self.G(name + ".weight"), self.G(name + ".bias"),
+                                    self.m.conv_pieces, 1, part=part)
 
     def wgrad(self, name, dy, x, KS, stride=1, pro=None):
         ps, ph = (None, None) if pro is None else pro
@@ -693,8 +697,8 @@ class _Exec:
         if bnb is not None:
             return self.dgrad(name, dy, res=res, out=out), None
         if ws is not None:
-            if ws.npieces == 3:
-                ys = Kn.split_activation(dy, 3, (ws.shape[1] == 9) * 1)
+            if ws.npieces in (1, 3):
+                ys = Kn.split_activation(dy, ws.npieces, (ws.shape[1] == 9) * 1)
                 return Kn.conv2d_forward_psa(ys, ws, None, res=res, out=out)
             return Kn.conv2d_forward_split(dy, ws, None, res=res, out=out)
         w = self.m.P(name + ".weight")
@@ -714,7 +718,7 @@ class _Exec:
         ws = self.m.SW(1, p + ".conv2.conv.weight")
         xs = self.saved_split.get(p + ".conv2.conv")
         cb = 64 if _WGRAD3_64 else 128
-        split_wgrad = (ws is not None and ws.npieces == 3 and xs is not None and t2.shape[1] % cb == 0
+        split_wgrad = (ws is not None and ws.npieces in (1, 3) and xs is not None and t2.shape[1] % cb == 0
                        and xs.C % cb == 0 and t2.shape[3] % 16 == 0)
         bwd2, part2 = self.bwd_epi(p + ".bn2", t1)
         if split_wgrad:
@@ -722,10 +726,10 @@ class _Exec:
             ys = self.bn_bwd_split(p + ".bn3", d, t2, relu=1, part=part)
             Kn.conv2d_wgrad3_psa(ys, xs, self.G(p + ".conv2.conv.weight"), self.G(p + ".conv2.conv.bias"))
             d = Kn.conv2d_forward_psa(ys, ws, None, bwd=bwd2)         # d relu(bn2(t1))
-        elif ws is not None and ws.npieces == 3:
+        elif ws is not None and ws.npieces in (1, 3):
             d = self.bn_bwd(p + ".bn3", d, t2, relu=1, part=part)     # d t2
             self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
-            d = Kn.conv2d_forward_psa(Kn.split_activation(d, 3, 1), ws, None, bwd=bwd2)
+            d = Kn.conv2d_forward_psa(Kn.split_activation(d, ws.npieces, 1), ws, None, bwd=bwd2)
         else:
             d = self.bn_bwd(p + ".bn3", d, t2, relu=1, part=part)     # d t2
             self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
