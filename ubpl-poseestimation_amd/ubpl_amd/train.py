@@ -588,6 +588,44 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
     return packed, (nf, mtc_n, B, len(cn), use_ep)
 
 
+class _LaggedRecords:
+    """A step's records reach the host one step late: the device->host copy of
+    step k goes into pinned memory asynchronously right behind step k's work,
+    and the host reads it (waiting on its event) only after step k+1 has been
+    enqueued — so the GPU never idles while the host enqueues the next step
+    (a blocking .cpu() per step drained the queue every step: the next step's
+    ~5k launches then started from an empty queue).  The records, their order
+    and every printed line are those of the blocking form; `consume` runs in
+    step order.  UBPL_LAG_RECORDS=0: consume each step's records at once."""
+    _on = os.environ.get("UBPL_LAG_RECORDS", "1") != "0"
+
+    def __init__(self):
+        self.pending = None
+
+    def push(self, packed, consume):
+        dev_t = packed.detach().reshape(-1)
+        host = torch.empty(dev_t.shape, dtype=dev_t.dtype, pin_memory=True)
+        host.copy_(dev_t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        prev, self.pending = self.pending, (host, ev, consume)
+        if prev is not None:
+            self._run(prev)
+        if not self._on:
+            self.flush()
+
+    def flush(self):
+        prev, self.pending = self.pending, None
+        if prev is not None:
+            self._run(prev)
+
+    @staticmethod
+    def _run(item):
+        host, ev, consume = item
+        ev.synchronize()
+        consume(host.tolist())
+
+
 def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
     """projects/MT_UBPL.py:157-352 -> (pec_records, mtc_records, epc_records, fdc_record).
     Steps after the first two are replayed from a captured HIP graph when the
@@ -603,28 +641,37 @@ def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
     for e in models_ema:
         e.train()
     runner = _StepGraph.get(_mt_ubpl_core, models, models_ema, optims, args)
+    lag = _LaggedRecords()
     for bat, (augs_imgMap, augs_heatmaps, meta) in enumerate(trainLoader):
-        packed, (nf, mtc_n, B, ncn, use_ep) = runner.run((augs_imgMap, augs_heatmaps, meta), dev)
-        host = packed.cpu().tolist()                              # the step's one device->host copy
-        nrec = 3 * M + 1
-        for mi in range(M):
-            pec_c[mi].update(host[3 * mi], int(host[nrec + 3 * mi]))
-            mtc_c[mi].update(host[3 * mi + 1], mtc_n)
-            # useEnsemblePseudo False: epc_counter.update(0., outs.shape[2]) (:292-293; outs.shape[2] = B)
-            epc_c[mi].update(host[3 * mi + 2], int(host[nrec + 3 * mi + 1]) if use_ep else B)
-        if nf:
-            fdc_c.update(host[3 * M], int(sum(host[nrec + 3 * M:nrec + 3 * M + nf])))
-        else:
-            fdc_c.update(0., B)
-        if verbose and use_ep:
-            n_ps = int(sum(host[nrec + 3 * mi + 1] for mi in range(M)))
-            n_sel = int(sum(host[nrec + 3 * mi + 2] for mi in range(M)))
-            sc = host[nrec + ncn:]
-            print("batch.{} (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
-                format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
-                format(n_sel / n_ps if n_ps else float("nan"), ".2f"), format(n_sel, "5d"), format(n_ps, "5d"),
-                ", ".join(format(v, ".3f") for v in sc)))
+        packed, meta_h = runner.run((augs_imgMap, augs_heatmaps, meta), dev)
+        # the step's one device->host copy, read after the next step is enqueued
+        lag.push(packed, lambda host, bat=bat, meta_h=meta_h: _mt_ubpl_records(
+            host, bat, meta_h, M, pec_c, mtc_c, epc_c, fdc_c, args, verbose))
+    lag.flush()
     return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
+
+
+def _mt_ubpl_records(host, bat, meta_h, M, pec_c, mtc_c, epc_c, fdc_c, args, verbose):
+    """One MT_UBPL step's host records -> the AvgCounters and the batch line."""
+    nf, mtc_n, B, ncn, use_ep = meta_h
+    nrec = 3 * M + 1
+    for mi in range(M):
+        pec_c[mi].update(host[3 * mi], int(host[nrec + 3 * mi]))
+        mtc_c[mi].update(host[3 * mi + 1], mtc_n)
+        # useEnsemblePseudo False: epc_counter.update(0., outs.shape[2]) (:292-293; outs.shape[2] = B)
+        epc_c[mi].update(host[3 * mi + 2], int(host[nrec + 3 * mi + 1]) if use_ep else B)
+    if nf:
+        fdc_c.update(host[3 * M], int(sum(host[nrec + 3 * M:nrec + 3 * M + nf])))
+    else:
+        fdc_c.update(0., B)
+    if verbose and use_ep:
+        n_ps = int(sum(host[nrec + 3 * mi + 1] for mi in range(M)))
+        n_sel = int(sum(host[nrec + 3 * mi + 2] for mi in range(M)))
+        sc = host[nrec + ncn:]
+        print("batch.{} (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
+            format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
+            format(n_sel / n_ps if n_ps else float("nan"), ".2f"), format(n_sel, "5d"), format(n_ps, "5d"),
+            ", ".join(format(v, ".3f") for v in sc)))
 
 
 def _fdl_rows(sw, args):
@@ -651,6 +698,7 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
         m.train()
     for e in models_ema:
         e.train()
+    lag = _LaggedRecords()
     for bat, (stu_imgMap, stu_heatmap, ema_imgMap, meta) in enumerate(trainLoader):
         for o in optims:
             o.zero_grad()
@@ -725,36 +773,43 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
                       args.consWeight * _norm(gsums[3 * mi], gcounts[6 * mi]),
                       args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else zero]
         g_rec.append(_fdl_record(fd, gsums[3 * M:], gcounts[6 * M:], W, args.FDLWeight) if fd else zero)
-        host = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, torch.stack(cons_sc).mean(0),
-                          torch.stack(ps_sc).mean(0) if use_ep else torch.zeros(K, device=dev)]).cpu().tolist()
-        nrec = 3 * M + 1
-        cbase = nrec
-        for mi in range(M):
-            pec_c[mi].update(host[3 * mi], int(host[cbase + 6 * mi + 1]))
-            mtc_c[mi].update(host[3 * mi + 1], int(host[cbase + 6 * mi]))
-            # useEnsemblePseudo False: epc_counter.update(0., outs.shape[2]) (:244-245; outs.shape[2] = nStack)
-            epc_c[mi].update(host[3 * mi + 2], int(host[cbase + 6 * mi + 2]) if use_ep else S)
-        if fd:
-            fdc_c.update(host[3 * M], int(host[cbase + 6 * M]))
-        else:
-            fdc_c.update(0., S)                                   # :249 outs.shape[2] = nStack
-        if verbose:
-            off = cbase + len(cn)
-            c_ps = int(sum(host[cbase + 6 * mi + 3] for mi in range(M)))
-            c_sel = int(sum(host[cbase + 6 * mi + 4] for mi in range(M)))
-            e_ps = int(sum(host[cbase + 6 * mi + 2] for mi in range(M)))
-            e_sel = int(sum(host[cbase + 6 * mi + 5] for mi in range(M)))
-            print("batch.{} consist-pseudo (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
-                format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
-                format(c_sel / c_ps if c_ps else float("nan"), ".2f"), format(c_sel, "5d"), format(c_ps, "5d"),
-                ", ".join(format(v, ".3f") for v in host[off:off + K])))
-            if use_ep:
-                print("batch.{} ensemble-pseudo (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
-                    format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
-                    format(e_sel / e_ps if e_ps else float("nan"), ".2f"), format(e_sel, "5d"), format(e_ps, "5d"),
-                    ", ".join(format(v, ".3f") for v in host[off + K:off + 2 * K])))
+        packed = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, torch.stack(cons_sc).mean(0),
+                            torch.stack(ps_sc).mean(0) if use_ep else torch.zeros(K, device=dev)])
+        lag.push(packed, lambda host, bat=bat, ncn=len(cn), K=K, use_ep=use_ep, nfd=len(fd): _dualpose_records(
+            host, bat, ncn, K, use_ep, nfd, M, S, pec_c, mtc_c, epc_c, fdc_c, args, verbose))
         del outs, outs_ema, feats, totals
+    lag.flush()
     return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
+
+
+def _dualpose_records(host, bat, ncn, K, use_ep, nfd, M, S, pec_c, mtc_c, epc_c, fdc_c, args, verbose):
+    """One DualPose_UBPL step's host records -> the AvgCounters and the batch lines."""
+    nrec = 3 * M + 1
+    cbase = nrec
+    for mi in range(M):
+        pec_c[mi].update(host[3 * mi], int(host[cbase + 6 * mi + 1]))
+        mtc_c[mi].update(host[3 * mi + 1], int(host[cbase + 6 * mi]))
+        # useEnsemblePseudo False: epc_counter.update(0., outs.shape[2]) (:244-245; outs.shape[2] = nStack)
+        epc_c[mi].update(host[3 * mi + 2], int(host[cbase + 6 * mi + 2]) if use_ep else S)
+    if nfd:
+        fdc_c.update(host[3 * M], int(host[cbase + 6 * M]))
+    else:
+        fdc_c.update(0., S)                                   # :249 outs.shape[2] = nStack
+    if verbose:
+        off = cbase + ncn
+        c_ps = int(sum(host[cbase + 6 * mi + 3] for mi in range(M)))
+        c_sel = int(sum(host[cbase + 6 * mi + 4] for mi in range(M)))
+        e_ps = int(sum(host[cbase + 6 * mi + 2] for mi in range(M)))
+        e_sel = int(sum(host[cbase + 6 * mi + 5] for mi in range(M)))
+        print("batch.{} consist-pseudo (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
+            format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
+            format(c_sel / c_ps if c_ps else float("nan"), ".2f"), format(c_sel, "5d"), format(c_ps, "5d"),
+            ", ".join(format(v, ".3f") for v in host[off:off + K])))
+        if use_ep:
+            print("batch.{} ensemble-pseudo (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
+                format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
+                format(e_sel / e_ps if e_ps else float("nan"), ".2f"), format(e_sel, "5d"), format(e_ps, "5d"),
+                ", ".join(format(v, ".3f") for v in host[off + K:off + 2 * K])))
 
 
 # ---------------------------------------------------------------------------
