@@ -20,7 +20,11 @@ def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     B, H = 32, 64
-    for cin, cout, resid in ((256, 128, False), (128, 256, True)):
+    shapes = ((256, 128, False), (128, 256, True))
+    if os.environ.get("SHAPE"):
+        shapes = (shapes[int(os.environ["SHAPE"])],)
+    only_sol = os.environ.get("ONLY_SOL") == "1"
+    for cin, cout, resid in shapes:
         x = torch.randn(B, cin, H, H, device=dev, generator=g)
         w = torch.randn(cout, cin, 1, 1, device=dev, generator=g) * 0.05
         b = torch.randn(cout, device=dev, generator=g)
@@ -31,7 +35,7 @@ def main():
         wk = Kn.conv_weight_flip(w)
         ws = Kn.conv_weight_split(w, 0, 3)
         torch.cuda.synchronize()
-        for _ in range(REPS):
+        for _ in range(0 if only_sol else REPS):
             Kn.conv1x1_forward_kmajor(x, wk, b, ps, ph, res=res, out=y)
         for _ in range(REPS):
             Kn.conv1x1_forward_split_load(x, ws, b, ps, ph, res=res, out=y)

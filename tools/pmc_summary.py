@@ -31,7 +31,7 @@ def main():
     d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
     out = sys.argv[2] if len(sys.argv) > 2 else None
     res = {}
-    for pas in ("sq", "fetch", "write"):
+    for pas in ("sq", "sq2", "fetch", "write"):
         f = os.path.join(d, pas + "_counter_collection.csv")
         if not os.path.exists(f):
             continue
