@@ -292,6 +292,8 @@ SOL_CASES = [
     (5, 256, 8, 256, False, True),
     (3, 128, 6, 128, True, False),
     (16, 128, 64, 256, True, True),       # 256-row 8-wave tiles (one pixel tile per CU)
+    (32, 256, 64, 128, True, True),       # the headline 64x64 level: 512-pixel 8-wave tiles, 3-stage ring
+    (37, 256, 60, 128, True, False),      # the same with a pixel tail (N % 512 = 80)
 ]
 
 
@@ -322,6 +324,10 @@ def test_conv1x1_split_load_vs_f64(case):
     e32, esp = _rel(y_f32, yref), _rel(y, yref)
     print("sol fwd %s: f32 %.2e split-load %.2e" % (case, e32, esp))
     assert esp <= 2 * e32 + 1e-8, (esp, e32)
+    # without the partials epilogue (the 512-pixel 3-stage kernel where it fills
+    # the chip): the same K order and chunking, so the same bits
+    y2 = Kn.conv1x1_forward_split_load(d(x32), Kn.conv_weight_split(d(w32), 0, 3), d(b32), ps, ph, res=d(res32))
+    assert torch.equal(y2, y)
     # BN statistics from the epilogue partials
     gamma, beta = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
     rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)

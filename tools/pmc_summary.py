@@ -19,7 +19,7 @@ def load(path):
     dur = collections.defaultdict(dict)
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        if "conv_" not in name:
+        if "conv" not in name:
             continue
         key = name.replace("void (anonymous namespace)::", "").split("(")[0]
         per[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
