@@ -511,6 +511,13 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
         const int cur = t % NS;
         const char* base = lds + cur * (AB + BB);
         bf16x8 af[TM][NP], bfr[TN][NP];
+        auto read_b = [&](int j) {
+            const int row = wn + 32 * j + li;
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                bfr[j][p] = *reinterpret_cast<const bf16x8*>(base + AB + p * BNT * 32 + row * 32 +
+                                                            16 * (h ^ ((row >> 3) & 1)));
+        };
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int row = wm + 32 * i + li;
@@ -518,23 +525,30 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             for (int p = 0; p < NP; ++p)
                 af[i][p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
         }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int row = wn + 32 * j + li;
-#pragma unroll
-            for (int p = 0; p < NP; ++p)
-                bfr[j][p] = *reinterpret_cast<const bf16x8*>(base + AB + p * BNT * 32 + row * 32 +
-                                                            16 * (h ^ ((row >> 3) & 1)));
-        }
         if constexpr (NP == 3 && TN > 2) {
-            // (no register room for every tile's chunk at once)
+            // (no register room for every tile's chunk at once)  The B fragments
+            // come in two halves: 18 reads in flight overflow the 4-bit lgkm
+            // counter and the compiler then waits for ALL of them before the first
+            // MFMA; with A + half of B (12) it waits for the first tile's operands
+            // only, and the second half is read behind the first column's MFMAs.
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+            for (int j = 0; j < TN / 2; ++j) read_b(j);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int j = 0; j < TN; ++j) {
+            for (int i = 0; i < TM; ++i) acc[i][0] += mfma_split0<NP>(af[i], bfr[0]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = TN / 2; j < TN; ++j) read_b(j);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 1; j < TN; ++j)
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
                     acc[i][j] += mfma_split0<NP>(af[i], bfr[j]);
                 }
         } else if constexpr (NP == 3) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) read_b(j);
             // every tile's chunk chain first, the f32 adds after them (behind a
             // scheduling barrier): an add right behind its own chain waits out
             // the MFMA latency (s_nop) with the other tiles' chains not issued
@@ -551,6 +565,8 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] += tmp[i][j];
         } else {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) read_b(j);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1666,10 +1682,18 @@ bool sol_supported(int B, int Cin, int Cout, int P) {
 
 // 1 when ubpl_conv1x1_forward_split_load takes this shape and fills the chip
 // (>= one 256-pixel workgroup per CU); 0: use the f32 1x1 kernel (split-K plans).
+// Output-channel block: 128 rows (each pixel tile split once per 128 channels)
+// unless that leaves CUs idle; then 64 (the 32x32-plane 256->128 convs at B=32:
+// 128 -> 256 workgroups).
+static int sol_bm(int64_t N, int Cout) {
+    if (Cout % 128 != 0) return 64;
+    return ((N + 255) / 256) * (Cout / 128) >= occ_info().ncu ? 128 : 64;
+}
+
 UBPL_API int ubpl_conv1x1_split_load_preferred(int B, int Cin, int Cout, int P) {
     if (!sol_supported(B, Cin, Cout, P)) return 0;
-    const int64_t bm = Cout % 128 == 0 ? 128 : 64;
-    const int64_t wgs = (((int64_t)B * P + 255) / 256) * (Cout / bm);
+    const int64_t N = (int64_t)B * P;
+    const int64_t wgs = ((N + 255) / 256) * (Cout / sol_bm(N, Cout));
     return wgs >= occ_info().ncu ? 1 : 0;
 }
 
@@ -1689,7 +1713,7 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
         return (int)hipErrorInvalidValue;
     const bool pro = pscale != nullptr;
     const int64_t N = (int64_t)B * P;
-    const int bm = Cout % 128 == 0 ? 128 : 64;
+    const int bm = sol_bm(N, Cout);
     const ubpl::BnBwdEpi bwd{bn_part ? bn_x : nullptr, bn_coef, bn_relu, bn_part};
     dim3 grid((unsigned)((N + 255) / 256), (unsigned)(Cout / bm));
     const bool epi = stat_part != nullptr || bn_part != nullptr;

@@ -16,8 +16,10 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libubpl_hip.so")
-OPS_PATH = os.path.join(_HERE, "libubpl_ops.so")
+# UBPL_LIB_DIR: another build of the same two libraries (same-box A/B of a kernel change)
+_LIB_DIR = os.environ.get("UBPL_LIB_DIR") or _HERE
+LIB_PATH = os.path.join(_LIB_DIR, "libubpl_hip.so")
+OPS_PATH = os.path.join(_LIB_DIR, "libubpl_ops.so")
 
 P, I, L, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_double
 
