@@ -6,8 +6,8 @@ OLD=${OLD:-$GRAFT_REPO_ROOT/build/ab_old}
 for r in 1 2; do
   for v in new old; do
     if [ $v = old ]; then e="UBPL_LIB_DIR=$OLD"; else e=""; fi
-    env $e timeout -k 10 120 python tools/psa_bench.py 32 50 > gpurun_out/ab_psa_$v.log 2>&1 || { tail -3 gpurun_out/ab_psa_$v.log; exit 1; }
-    echo "psa $v r$r: $(grep -E 'B=' gpurun_out/ab_psa_$v.log | head -4 | cut -c1-75 | tr '\n' ' ')"
+    env $e timeout -k 10 200 ${MB:-python tools/psa_bench.py 32 50} > gpurun_out/ab_mb_$v.log 2>&1 || { tail -3 gpurun_out/ab_mb_$v.log; exit 1; }
+    echo "== microbench $v r$r"; grep -E "${MB_GREP:-B=}" gpurun_out/ab_mb_$v.log | head -${MB_LINES:-4} | cut -c1-90
   done
 done
 for r in 1 2; do
