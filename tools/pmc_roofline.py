@@ -9,9 +9,10 @@ so it is doubled.  Writes profiles/pmc_roofline.json for bench.py.
 
     python tools/pmc_roofline.py gpurun_out/pmc_bench profiles/pmc_roofline.json [source-tag] [f32|psa]
 
-With "psa" (conv precision 6xbf16) the roofline kernel is conv_psa_kernel<BM, 3, 3>:
-every 3x3 launch of it, forward and data gradient (same shapes, same traffic
-model; rocprof names cannot tell them apart).
+With "psa" (conv precision 6xbf16) the roofline kernel is bench.py's:
+conv_psa_kernel<128, 3, 3, 256, 2> on 512-workgroup grids (the 128 -> 128
+3x3 convs on the 64x64 planes at B=32, forward and data gradient: rocprof
+names cannot tell them apart, same shapes and traffic model).
 """
 import csv
 import json
@@ -20,14 +21,19 @@ import re
 import sys
 
 PATS = {"f32": re.compile(r"conv_fwd_kernel<(\d+), 128, 3, 1, true, false"),
-        "psa": re.compile(r"conv_psa_kernel<(\d+), 3, 3(, \d+, \d+)?>")}
+        "psa": re.compile(r"conv_psa_kernel<128, 3, 3, 256, 2(, false)?>")}
+# psa: only the 512-workgroup launches (grid size in work-items)
+GRID = {"psa": 512 * 256}
 PAT = PATS["f32"]
+KIND = "f32"
 
 
 def per_launch(path, counter):
     vals = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter or not PAT.search(r["Kernel_Name"]):
+            continue
+        if GRID.get(KIND) and int(r["Grid_Size"]) != GRID[KIND]:
             continue
         vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return vals
@@ -38,15 +44,16 @@ def main():
     out = sys.argv[2]
     tag = sys.argv[3] if len(sys.argv) > 3 else d
     kind = sys.argv[4] if len(sys.argv) > 4 else "f32"
-    global PAT
-    PAT = PATS[kind]
+    global PAT, KIND
+    PAT, KIND = PATS[kind], kind
     fetch = per_launch(os.path.join(d, "fetch_counter_collection.csv"), "FETCH_SIZE")
     write = per_launch(os.path.join(d, "write_counter_collection.csv"), "WRITE_SIZE")
     nf, nw = len(fetch), len(write)
     fb = 2 * 1024 * sum(fetch.values()) / max(nf, 1)
     wb = 1024 * sum(write.values()) / max(nw, 1)
     res = {"kernel": ("conv_fwd_kernel<*,128,3,1,PRO> (all launches of the bench step)" if kind == "f32" else
-                      "conv_psa_kernel<*,3,3> (all 3x3 launches of the bench step: forward + data gradient)"),
+                      "conv_psa_kernel<128, 3, 3, 256, 2> on 512-workgroup grids (3x3 128->128 at 64x64, "
+                      "B=32: forward + data gradient)"),
            "launches_fetch_pass": nf, "launches_write_pass": nw,
            "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
            "hbm_bytes_per_launch": fb + wb,
