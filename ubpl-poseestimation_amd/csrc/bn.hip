@@ -91,6 +91,38 @@ struct StatsOut {
 // One (channel c, batch slice) per block over the flattened (b, pixel) range:
 // sum and sum of squares of (x - x0), x0 = x[0, c, 0]; f32 per thread, f64
 // across the block and the slices.  The last block of channel c finalizes it.
+// Visits the float4 offsets of channel c over images [b0, b1) of an NCHW
+// tensor (hw4 float4s per plane, 256-thread blocks), calling f(slot, offset)
+// (slot = the position in a group of U).  When every plane is whole
+// 256-float4 rows (hw4 = 256 * 2^k: the 32x32 planes and up) each thread walks
+// the same elements in the same order as the flattened (image, offset) loop,
+// with no index division and U independent loads in flight; otherwise that loop.
+template <int U, typename F>
+__device__ __forceinline__ void visit_chan4(int b0, int b1, int C, int c, int hw4, F&& f) {
+    const int kq = hw4 >> 8;
+    if ((hw4 & 255) == 0 && (kq & (kq - 1)) == 0) {
+        const int ksh = __builtin_ctz(kq);
+        const int nj = (b1 - b0) << ksh;
+        const int64_t bstride = (int64_t)C * hw4;
+        const int64_t base = ((int64_t)b0 * C + c) * hw4 + threadIdx.x;
+        int j = 0;
+        for (; j + U <= nj; j += U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int jj = j + u;
+                f(u, base + (int64_t)(jj >> ksh) * bstride + ((int64_t)(jj & (kq - 1)) << 8));
+            }
+        }
+        for (; j < nj; ++j) f(0, base + (int64_t)(j >> ksh) * bstride + ((int64_t)(j & (kq - 1)) << 8));
+        return;
+    }
+    const int n4 = (b1 - b0) * hw4;
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+        const int bb = i / hw4, o4 = i - bb * hw4;
+        f(0, ((int64_t)(b0 + bb) * C + c) * hw4 + o4);
+    }
+}
+
 template <bool VEC>
 __global__ void __launch_bounds__(256) stats_kernel(const float* __restrict__ x, int B, int C, int HW, int bper,
                                                    double* __restrict__ part, unsigned* __restrict__ cnt,
@@ -101,16 +133,15 @@ __global__ void __launch_bounds__(256) stats_kernel(const float* __restrict__ x,
     const float x0 = x[(int64_t)c * HW];
     float s1 = 0.f, s2 = 0.f;
     if (VEC) {
-        const int hw4 = HW >> 2;
-        const int n4 = (b1 - b0) * hw4;
+        // one accumulator, elements in the flattened loop's order (bit-identical
+        // statistics); only the loads run ahead
         const float4* x4 = reinterpret_cast<const float4*>(x);
-        for (int i = threadIdx.x; i < n4; i += blockDim.x) {
-            const int bb = i / hw4, o4 = i - bb * hw4;
-            const float4 v = x4[((int64_t)(b0 + bb) * C + c) * hw4 + o4];
+        visit_chan4<4>(b0, b1, C, c, HW >> 2, [&](int, int64_t off) {
+            const float4 v = x4[off];
             const float a = v.x - x0, q = v.y - x0, r = v.z - x0, d = v.w - x0;
             s1 += (a + q) + (r + d);
             s2 = fmaf(a, a, fmaf(q, q, fmaf(r, r, fmaf(d, d, s2))));
-        }
+        });
     } else {
         const int n = (b1 - b0) * HW;
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -204,6 +235,7 @@ __global__ void __launch_bounds__(256) bwd_stats_kernel(const float* __restrict_
     const float sc = scale[c], sh = shift[c], mu = mean[c];
     float s1 = 0.f, s2 = 0.f;
     if (VEC) {
+        // (visit_chan4 here measured 7 % slower: the flattened loop stays)
         const int hw4 = HW >> 2;
         const int n4 = (b1 - b0) * hw4;
         const float4* x4 = reinterpret_cast<const float4*>(x);
