@@ -175,7 +175,12 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step):
     flops = 2 * B * Cout * Cin * KS * KS * H * W
     achieved = flops / (avg_ms * 1e-3) / 1e12
     per_step_ms = n * avg_ms
-    assert per_step_ms <= ms_per_step, (per_step_ms, ms_per_step)
+    # standalone replays summed vs the measured step: a check, reported (never an abort after the
+    # timed region — box noise, or in-situ overlap making the step shorter than serial launches)
+    consistent = per_step_ms <= ms_per_step
+    if not consistent:
+        print("bench: roofline kernel replays sum to %.2f ms > %.2f ms/step" % (per_step_ms, ms_per_step),
+              file=sys.stderr)
     pmc = pmc_traffic("psa")
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(SPLIT6_PEAK_TFLOPS, 2),
             "unit": "TFLOP/s", "frac": round(achieved / SPLIT6_PEAK_TFLOPS, 4),
@@ -183,7 +188,7 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step):
             "kernel": "conv_psa_kernel<128, 3, 3, 256, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
                       "6xbf16 split-f32 MFMA; f32-equivalent FLOP/s, peak = bf16 dense / 6)",
             "flops_per_launch": flops, "launches_per_step": n, "avg_launch_us": round(avg_ms * 1e3, 2),
-            "kernel_ms_per_step": round(per_step_ms, 3),
+            "kernel_ms_per_step": round(per_step_ms, 3), "fits_in_step": consistent,
             "timing": "HIP events around back-to-back replays of the step's launches of this kernel "
                       "(standalone; inputs resident), after the timed region"}
 
@@ -233,7 +238,7 @@ def cpu_baseline(steps=1, B=32):
     from oracle import hourglass as OH
     from oracle import render as OR
     from oracle import step as OS
-    threads = int(os.environ.get("UBPL_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    threads = int(os.environ.get("UBPL_CPU_THREADS", min(8, os.cpu_count() or 1)))
     torch.set_num_threads(threads)
     torch.manual_seed(1388)
     models, emas, optims = [], [], []
@@ -260,14 +265,22 @@ def cpu_baseline(steps=1, B=32):
     t = time.time()
     OS.train_mt_ubpl(batches, models, emas, optims, args)
     dt = time.time() - t
-    cal = os.path.join(ROOT, "profiles", "r02_cpu_calibration_b32.json")
-    ratio = json.load(open(cal))["port_over_reference"] if os.path.exists(cal) else None
+    cal = os.path.join(ROOT, "profiles", "r03_cpu_calibration_b32.json")
+    ratio, cal_threads = None, None
+    if os.path.exists(cal):
+        with open(cal) as fh:
+            c = json.load(fh)
+        ratio, cal_threads = c["port_over_reference"], c.get("threads")
+    # the port/reference ratio holds at the thread count it was measured with only
+    pinned = ratio is not None and cal_threads == threads
     return {"value": round(steps * B / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "reference_equivalent": round(steps * B / dt / ratio, 4) if ratio else None,
-            "port_over_reference": ratio,
+            "reference_equivalent": round(steps * B / dt / ratio, 4) if pinned else None,
+            "port_over_reference": ratio, "calibration_threads": cal_threads,
+            "calibration": "pinned" if pinned else "unpinned (calibrated at %s threads, run at %d)"
+                           % (cal_threads, threads),
             "sample": "oracle/step.py MT_UBPL step (same math as projects/MT_UBPL.py:157-352), 2-stack, "
                       "B=%d (half labeled), 256x256, K=16, %d timed step(s) = %.1f s, torch CPU fp32; "
-                      "calibration vs the reference train(): profiles/r02_cpu_calibration_b4.json, _b32.json"
+                      "calibration vs the reference train(): profiles/r03_cpu_calibration_b32.json"
                       % (B, steps, dt)}
 
 

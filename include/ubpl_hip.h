@@ -11,7 +11,15 @@
  *   - layouts are the reference's: NCHW float32 tensors, contiguous.
  *
  * Reference interfaces replaced (paths relative to the reference root) are
- * cited per entry.  The Python host layer (ubpl-poseestimation_amd/ubpl_amd)
+ * cited per entry.
+ *
+ * Argument annotations: the comment `/ *@ name:type[extent] ... * /` right
+ * before a declaration gives each pointer argument its element type (f32,
+ * f64, i32, i64, u16 = bf16 pieces, u8) and the number of elements the call
+ * may touch, as a C expression of the integer arguments ("?" = not derivable
+ * from them).  csrc/gen_torch_ops.py turns them into the torch ops' argument
+ * checks (dtype, contiguity, storage extent), so a short tensor raises there
+ * instead of being written out of bounds.  The Python host layer (ubpl-poseestimation_amd/ubpl_amd)
  * binds these through ctypes and re-exposes the reference's module API.
  */
 #ifndef UBPL_HIP_H
@@ -27,6 +35,7 @@ extern "C" {
  * kps [N,K,3] (x, y, vis) in image pixels -> hm [N,K,size_h,size_w] with
  * size = int(img / (inp_res/out_res)); kps_out[...,2] = vis * visible
  * (may alias kps: the reference mutates kpsMap in place, :267). */
+/*@ kps:f32[N*K*3] hm:f32[(int64_t)N*K*(int)(img_h/((double)inp_res/out_res))*(int)(img_w/((double)inp_res/out_res))] kps_out:f32[N*K*3] */
 int ubpl_render_heatmaps(const float* kps, float* hm, float* kps_out, int N, int K, int img_h, int img_w,
                          int inp_res, int out_res, float kernel_size, float sigma, float cutoff, void* stream);
 
@@ -36,6 +45,7 @@ int ubpl_render_heatmaps(const float* kps, float* hm, float* kps_out, int N, int
  * Outputs [B*S*K]: sq_mean; amax = max_px a (nullable); tmax = max_px target (nullable).
  * JointMSELoss / JointDistLoss / JointDistLoss_mt2 / JointPseudoLoss3 forward
  * (utils/losses.py:16-53, 255-286, 176-210). */
+/*@ a:f32[(B-1)*a_sb+(S-1)*a_ss+(int64_t)K*HW] t:f32[(M-1)*t_sm+(B-1)*t_sb+(S-1)*t_ss+(int64_t)K*HW] sq_mean:f32[B*S*K] amax:f32[B*S*K] tmax:f32[B*S*K] */
 int ubpl_heatmap_row_stats(const float* a, int64_t a_sb, int64_t a_ss, const float* t, int64_t t_sb, int64_t t_ss,
                            int64_t t_sm, int M, int B, int S, int K, int HW, float* sq_mean, float* amax,
                            float* tmax, void* stream);
@@ -43,10 +53,12 @@ int ubpl_heatmap_row_stats(const float* a, int64_t a_sb, int64_t a_ss, const flo
  * confidence mask (mt2), 2 UBPL pseudo mask.  out_sum[1] f32; out_cnt[4] int32 =
  * {nStack*#gate>0, n_pseudo, n_sel, #rows sw>0}; out_score[K] (kinds 1,2);
  * out_w[B*S*K] per-row weight for the backward. */
+/*@ sq_mean:f32[B*S*K] amax:f32[B*S*K] tmax:f32[B*S*K] gate:f32[B*K] sw:f32[B] out_sum:f32[1] out_cnt:i32[4] out_score:f32[K] out_w:f32[B*S*K] */
 int ubpl_loss_finalize(int kind, const float* sq_mean, const float* amax, const float* tmax, const float* gate,
                        const float* sw, int use_gate, int use_sw, int B, int S, int K, float thr, float* out_sum,
                        int* out_cnt, float* out_score, float* out_w, void* stream);
 /* d a (+)= w_row * (*gscale) * extra * (a - target); gscale device scalar (nullable = 1). */
+/*@ a:f32[(B-1)*a_sb+(S-1)*a_ss+(int64_t)K*HW] t:f32[(M-1)*t_sm+(B-1)*t_sb+(S-1)*t_ss+(int64_t)K*HW] w:f32[B*S*K] gscale:f32[1] da:f32[(B-1)*a_sb+(S-1)*a_ss+(int64_t)K*HW] */
 int ubpl_heatmap_row_grad(const float* a, int64_t a_sb, int64_t a_ss, const float* t, int64_t t_sb, int64_t t_ss,
                           int64_t t_sm, int M, int B, int S, int K, int HW, const float* w, const float* gscale,
                           float extra, float* da, int accumulate, void* stream);
@@ -56,8 +68,10 @@ int ubpl_heatmap_row_grad(const float* a, int64_t a_sb, int64_t a_ss, const floa
  * rowmask[b] > 0 (the caller's labeled-row selection, projects/MT_UBPL.py:309-320).
  * f1,f2 [B,S,C,HW]; cov/mu1/mu2 [B*S*C] scratch; out_val[1] = mean |cov|;
  * out_cnt[1] = #selected * S * C. */
+/*@ f1:f32[(int64_t)B*S*C*HW] f2:f32[(int64_t)B*S*C*HW] rowmask:f32[B] cov:f32[B*S*C] mu1:f32[B*S*C] mu2:f32[B*S*C] out_val:f32[1] out_cnt:i32[1] */
 int ubpl_fdl_cov_forward(const float* f1, const float* f2, const float* rowmask, int B, int S, int C, int HW,
                          float* cov, float* mu1, float* mu2, float* out_val, int* out_cnt, void* stream);
+/*@ f1:f32[(int64_t)B*S*C*HW] f2:f32[(int64_t)B*S*C*HW] rowmask:f32[B] cov:f32[B*S*C] mu1:f32[B*S*C] mu2:f32[B*S*C] cnt:i32[1] gscale:f32[1] d1:f32[(int64_t)B*S*C*HW] d2:f32[(int64_t)B*S*C*HW] */
 int ubpl_fdl_cov_backward(const float* f1, const float* f2, const float* rowmask, const float* cov, const float* mu1,
                           const float* mu2, const int* cnt, const float* gscale, int B, int S, int C, int HW,
                           float* d1, float* d2, int accumulate, void* stream);
@@ -66,30 +80,37 @@ int ubpl_fdl_cov_backward(const float* f1, const float* f2, const float* rowmask
  * get_preds + final_preds + kps_fromHeatmap (utils/udaap/evaluation.py:13-30,215-238;
  * utils/process.py:320-327).  tinv [N,6] f64 = rows 0-1 of inv(get_transform)
  * (nullable: no transform).  raw/preds [N,K,2], scores [N,K] (each nullable). */
+/*@ hm:f32[(int64_t)N*K*H*W] tinv:f64[N*6] raw:f32[N*K*2] preds:f32[N*K*2] scores:f32[N*K] */
 int ubpl_decode_heatmaps(const float* hm, int N, int K, int H, int W, const double* tinv, float* raw, float* preds,
                          float* scores, void* stream);
 /* EvaluationUtils.acc_pck (utils/evaluation.py:91-139).  errs/accs [K+1];
  * hits/valid [K] int32 (nullable) for cross-rank aggregation. */
+/*@ preds:f32[N*K*2] gts:f32[N*K*3] errs:f32[K+1] accs:f32[K+1] hits:i32[K] valid:i32[K] */
 int ubpl_pck(const float* preds, const float* gts, int N, int K, int ref0, int ref1, float thr, float* errs,
              float* accs, int* hits, int* valid, void* stream);
 
 /* ---------------------------------------------------------------- E1 ----
  * update_ema_variables (utils/parameters.py:4-8) on a flat parameter buffer. */
+/*@ ema:f32[n] p:f32[n] */
 int ubpl_ema_update(float* ema, const float* p, int64_t n, double alpha, void* stream);
 /* torch.optim.AdamW step (the optimizer projects/MT_UBPL.py:48 builds) on flat buffers. */
+/*@ p:f32[n] g:f32[n] m:f32[n] v:f32[n] */
 int ubpl_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
                     double eps, double weight_decay, int64_t step, void* stream);
 /* The same step with the 1-based step count on the device (incremented by the
  * call), so a captured HIP graph of the training step replays it; coef: 4 floats. */
+/*@ p:f32[n] g:f32[n] m:f32[n] v:f32[n] step:i64[1] coef:f32[4] */
 int ubpl_adamw_step_dev(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1,
                         double beta2, double eps, double weight_decay, int64_t* step, float* coef, void* stream);
 /* ubpl_adamw_step_dev on p[0, nlive) fused with ubpl_ema_update(ema, p, n) in
  * one pass (the optimizer step of projects/MT_UBPL.py:338-340 followed by
  * update_ema_variables, utils/parameters.py:4-8); bit-identical to the two
  * calls.  nlive, n multiples of 4; buffers 16-B aligned. */
+/*@ p:f32[n] g:f32[nlive] m:f32[nlive] v:f32[nlive] step:i64[1] coef:f32[4] ema:f32[n] */
 int ubpl_adamw_ema_step_dev(float* p, const float* g, float* m, float* v, int64_t nlive, double lr, double beta1,
                             double beta2, double eps, double weight_decay, int64_t* step, float* coef, float* ema,
                             int64_t n, double alpha, void* stream);
+/*@ x:f32[n] */
 int ubpl_scale_(float* x, int64_t n, float s, void* stream);
 
 /* ---------------------------------------------------------------- H2-H4 --
@@ -100,11 +121,14 @@ int ubpl_scale_(float* x, int64_t n, float s, void* stream);
  * (nullable).  scale = gamma*invstd, shift = beta - mean*scale. */
 int ubpl_bn_splits(int B, int C);
 int64_t ubpl_bn_part_doubles(int B, int C);
+/*@ x:f32[(int64_t)B*C*HW] gamma:f32[C] beta:f32[C] rmean:f32[C] rvar:f32[C] part:f64[ubpl_bn_part_doubles(B,C)] mean_out:f32[C] invstd_out:f32[C] scale:f32[C] shift:f32[C] */
 int ubpl_bn_forward_stats(const float* x, int B, int C, int HW, const float* gamma, const float* beta, float eps,
                           float momentum, float* rmean, float* rvar, double* part, float* mean_out,
                           float* invstd_out, float* scale, float* shift, void* stream);
+/*@ gamma:f32[C] beta:f32[C] rmean:f32[C] rvar:f32[C] scale:f32[C] shift:f32[C] */
 int ubpl_bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
                         int C, float* scale, float* shift, void* stream);
+/*@ x:f32[(int64_t)B*C*HW] scale:f32[C] shift:f32[C] y:f32[(int64_t)B*C*HW] */
 int ubpl_bn_apply(const float* x, int B, int C, int HW, const float* scale, const float* shift, int relu, float* y,
                   void* stream);
 /* Statistics from 64-pixel partials: part [C][ceil(N/64)][2] f32 = (S, M2) =
@@ -113,7 +137,9 @@ int ubpl_bn_apply(const float* x, int B, int C, int HW, const float* scale, cons
  * accumulators (stat_part arguments), ubpl_bn_partials from a tensor.
  * ubpl_bn_stats_from_partials: outputs as ubpl_bn_forward_stats, f64 combine. */
 int64_t ubpl_bn_partial_floats(int C, int64_t N);
+/*@ y:f32[(int64_t)B*C*P] part:f32[ubpl_bn_partial_floats(C,(int64_t)B*P)] */
 int ubpl_bn_partials(const float* y, int B, int C, int P, float* part, void* stream);
+/*@ part:f32[ubpl_bn_partial_floats(C,N)] gamma:f32[C] beta:f32[C] rmean:f32[C] rvar:f32[C] mean_out:f32[C] invstd_out:f32[C] scale:f32[C] shift_out:f32[C] */
 int ubpl_bn_stats_from_partials(const float* part, int C, int64_t N, const float* gamma,
                                 const float* beta, float eps, float momentum, float* rmean, float* rvar,
                                 float* mean_out, float* invstd_out, float* scale, float* shift_out, void* stream);
@@ -124,6 +150,7 @@ int ubpl_bn_stats_from_partials(const float* part, int C, int64_t N, const float
  * (S1, S2) = (sum g, sum g*(x - mean)), g = dz under the recomputed ReLU mask,
  * ubpl_bn_partial_floats(C, B*HW) floats (a conv epilogue's bn_part argument,
  * or ubpl_bn_backward_partials); coef: 3*C floats of scratch. */
+/*@ dz:f32[(int64_t)B*C*HW] x:f32[(int64_t)B*C*HW] gamma:f32[C] mean:f32[C] invstd:f32[C] scale:f32[C] shift:f32[C] scratch:f64[ubpl_bn_part_doubles(B,C)] part:f32[ubpl_bn_partial_floats(C,(int64_t)B*HW)] coef:f32[3*C] dgamma:f32[C] dbeta:f32[C] add1:f32[(int64_t)B*C*HW] add2:f32[(int64_t)B*C*HW] dx:f32[(int64_t)B*C*HW] */
 int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, const float* gamma, const float* mean,
                      const float* invstd, const float* scale, const float* shift, int relu, double* scratch,
                      const float* part, float* coef, float* dgamma, float* dbeta, const float* add1,
@@ -131,11 +158,13 @@ int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, cons
 /* The same backward with dx delivered only as PSA planes (ubpl_split_activation
  * layout, border `pad`, npieces 2 or 3) — the operand of a split-path 3x3 data /
  * weight gradient; no addends; C % 16 == 0. */
+/*@ dz:f32[(int64_t)B*C*H*W] x:f32[(int64_t)B*C*H*W] gamma:f32[C] mean:f32[C] invstd:f32[C] scale:f32[C] shift:f32[C] scratch:f64[ubpl_bn_part_doubles(B,C)] part:f32[ubpl_bn_partial_floats(C,(int64_t)B*H*W)] coef:f32[3*C] dgamma:f32[C] dbeta:f32[C] dst:u16[(npieces-1)*plane+(int64_t)B*C*(H+2*pad)*(W+2*pad)] */
 int ubpl_bn_backward_split(const float* dz, const float* x, int B, int C, int H, int W, const float* gamma,
                            const float* mean, const float* invstd, const float* scale, const float* shift, int relu,
                            double* scratch, const float* part, float* coef, float* dgamma, float* dbeta, int pad,
                            int npieces, uint16_t* dst, int64_t plane, void* stream);
 /* The backward statistics partials alone (the layout above). */
+/*@ dz:f32[(int64_t)B*C*HW] x:f32[(int64_t)B*C*HW] scale:f32[C] shift:f32[C] mean:f32[C] part:f32[ubpl_bn_partial_floats(C,(int64_t)B*HW)] */
 int ubpl_bn_backward_partials(const float* dz, const float* x, int B, int C, int HW, const float* scale,
                               const float* shift, const float* mean, int relu, float* part, void* stream);
 
@@ -148,9 +177,11 @@ int ubpl_bn_backward_partials(const float* dz, const float* x, int B, int C, int
  * Small grids split K over workgroups: slab = ubpl_conv2d_forward_workspace
  * floats (nullable when that is 0). */
 int64_t ubpl_conv2d_forward_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo);
+/*@ x:f32[(int64_t)B*Cin*H*W] w:f32[(int64_t)Cout*Cin*KS*KS] bias:f32[Cout] pscale:f32[Cin] pshift:f32[Cin] res:f32[(int64_t)B*Cout*Ho*Wo] y:f32[(int64_t)B*Cout*Ho*Wo] slab:f32[ubpl_conv2d_forward_workspace(B,Cin,Cout,KS,Ho,Wo)] */
 int ubpl_conv2d_forward(const float* x, int B, int Cin, int H, int W, const float* w, const float* bias, int Cout,
                         int KS, int stride, const float* pscale, const float* pshift, const float* res, float* y,
                         int Ho, int Wo, float* slab, void* stream);
+/*@ w:f32[(int64_t)Cout*Cin*KS*KS] wt:f32[(int64_t)Cout*Cin*KS*KS] */
 int ubpl_conv_weight_tapmajor(const float* w, int Cout, int Cin, int KS, float* wt, void* stream);
 /* 1x1 stride-1 conv fed by LDS-DMA, k-major weights wk [Cin][Cout] (the
  * data-gradient re-layout of the conv; for a data gradient, the reference
@@ -158,24 +189,29 @@ int ubpl_conv_weight_tapmajor(const float* w, int Cout, int Cin, int KS, float* 
  * Cin % 16 == 0, Cout % 4 == 0, P % 4 == 0, x / wk 16-B aligned, Cin <= 256 with a
  * prologue. */
 int64_t ubpl_conv1x1_kmajor_workspace(int B, int Cin, int Cout, int P);
+/*@ x:f32[(int64_t)B*Cin*P] wk:f32[(int64_t)Cin*Cout] bias:f32[Cout] pscale:f32[Cin] pshift:f32[Cin] res:f32[(int64_t)B*Cout*P] y:f32[(int64_t)B*Cout*P] slab:f32[ubpl_conv1x1_kmajor_workspace(B,Cin,Cout,P)] stat_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*P)] */
 int ubpl_conv1x1_forward_kmajor(const float* x, int B, int Cin, int P, const float* wk, const float* bias, int Cout,
                                 const float* pscale, const float* pshift, const float* res, float* y, float* slab,
                                 float* stat_part, void* stream);
 /* Weight gradient (+ bias gradient), reference weight layout. */
 int64_t ubpl_conv2d_wgrad_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo);
+/*@ dy:f32[(int64_t)B*Cout*Ho*Wo] x:f32[(int64_t)B*Cin*H*W] pscale:f32[Cin] pshift:f32[Cin] slab:f32[ubpl_conv2d_wgrad_workspace(B,Cin,Cout,KS,Ho,Wo)] dw:f32[(int64_t)Cout*Cin*KS*KS] db:f32[Cout] */
 int ubpl_conv2d_wgrad(const float* dy, const float* x, int B, int Cin, int H, int W, int Cout, int KS, int stride,
                       const float* pscale, const float* pshift, int Ho, int Wo, float* slab, float* dw, float* db,
                       int accumulate, void* stream);
 /* Data-gradient weights (stride 1): the forward layout of the flipped,
  * transposed kernel ([Cin][Cout/G][T][G], G from Cout), so
  * dx = ubpl_conv2d_forward(dy, wt). */
+/*@ w:f32[(int64_t)Cout*Cin*KS*KS] wt:f32[(int64_t)Cout*Cin*KS*KS] */
 int ubpl_conv_weight_flip(const float* w, int Cout, int Cin, int KS, float* wt, void* stream);
 /* Reduce a weight-gradient slab [splits][Cout][Cin*T + 1] (columns n = tap*Cin + ci,
  * last = bias) into dw (reference layout, (+)=) and db (nullable). */
+/*@ slab:f32[(int64_t)splits*Cout*((int64_t)Cin*T+1)] dw:f32[(int64_t)Cout*Cin*T] db:f32[Cout] */
 int ubpl_wgrad_slab_reduce(const float* slab, int splits, int Cout, int Cin, int T, int with_bias, float* dw,
                            float* db, int accumulate, void* stream);
 /* Both re-layouts for many convs in one launch: table int64 [nseg][5] =
  * (src_off, dst_off, Cout, Cin, KS*KS) in floats; mode 0 tap-major, 1 dgrad. */
+/*@ src:f32[?] dst:f32[?] table:i64[nseg*5] */
 int ubpl_conv_weights_relayout(const float* src, float* dst, const int64_t* table, int nseg, int mode, void* stream);
 
 /* Split-bf16 MFMA path of the same Conv (conv_split.hip): every f32 operand
@@ -186,9 +222,11 @@ int ubpl_conv_weights_relayout(const float* src, float* dst, const int64_t* tabl
  * for many convs in one launch (table as above, dst_off % 8 == 0).
  * ubpl_conv2d_forward_split: (KS, stride) in {(1,1), (3,1)}, Cin % 16 == 0,
  * wsplit 16-B aligned; other arguments as ubpl_conv2d_forward. */
+/*@ src:f32[?] dst:u16[npieces*plane] table:i64[nseg*5] */
 int ubpl_conv_weights_split(const float* src, uint16_t* dst, int64_t plane, const int64_t* table, int nseg, int mode,
                             int npieces, void* stream);
 int64_t ubpl_conv2d_forward_split_workspace(int B, int Cin, int Cout, int KS, int Ho, int Wo, int npieces);
+/*@ x:f32[(int64_t)B*Cin*H*W] wsplit:u16[(npieces-1)*plane+(int64_t)Cout*Cin*KS*KS] bias:f32[Cout] pscale:f32[Cin] pshift:f32[Cin] res:f32[(int64_t)B*Cout*Ho*Wo] y:f32[(int64_t)B*Cout*Ho*Wo] slab:f32[ubpl_conv2d_forward_split_workspace(B,Cin,Cout,KS,Ho,Wo,npieces)] */
 int ubpl_conv2d_forward_split(const float* x, int B, int Cin, int H, int W, const uint16_t* wsplit, int64_t plane,
                               const float* bias, int Cout, int KS, int stride, const float* pscale,
                               const float* pshift, const float* res, float* y, int Ho, int Wo, float* slab,
@@ -196,6 +234,7 @@ int ubpl_conv2d_forward_split(const float* x, int B, int Cin, int H, int W, cons
 /* Pre-split activations ("PSA"): npieces bf16 planes (`plane` elements apart)
  * of [B][C/16][H+2pad][W+2pad][16] holding relu(x*pscale + pshift) (or x when
  * pscale is null) with a zero border; C % 16 == 0. */
+/*@ x:f32[(int64_t)B*C*H*W] pscale:f32[C] pshift:f32[C] dst:u16[(npieces-1)*plane+(int64_t)B*C*(H+2*pad)*(W+2*pad)] */
 int ubpl_split_activation(const float* x, int B, int C, int H, int W, const float* pscale, const float* pshift,
                           int pad, int npieces, uint16_t* dst, int64_t plane, void* stream);
 /* Stride-1 conv (KS 1 or 3) of PSA activations (pad >= (KS-1)/2) with split
@@ -205,6 +244,7 @@ int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int KS, int 
  * operands with a 1-pixel border: dys = split(dy), xs = split(conv input),
  * npieces = 3; Cin % 64 == 0, Cout % 64 == 0, W % 16 == 0. */
 int64_t ubpl_wgrad3_psa_workspace(int B, int Cin, int Cout, int H, int W);
+/*@ dys:u16[(npieces-1)*dplane+(int64_t)B*Cout*(H+2)*(W+2)] xs:u16[(npieces-1)*xplane+(int64_t)B*Cin*(H+2)*(W+2)] slab:f32[ubpl_wgrad3_psa_workspace(B,Cin,Cout,H,W)] dw:f32[(int64_t)Cout*Cin*9] db:f32[Cout] */
 int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int Cin,
                     int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,
                     void* stream);
@@ -213,8 +253,10 @@ int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int
  * pshift) when pscale != nullptr) split while staged.  _workspace: slab floats,
  * 0 = shape not supported (needs Cin % 128 == 0, Cout % 128 == 0, P % 16 == 0). */
 int64_t ubpl_wgrad1x1_split_load_workspace(int B, int Cin, int Cout, int P);
+/*@ dy:f32[(int64_t)B*Cout*P] x:f32[(int64_t)B*Cin*P] pscale:f32[Cin] pshift:f32[Cin] slab:f32[ubpl_wgrad1x1_split_load_workspace(B,Cin,Cout,P)] dw:f32[(int64_t)Cout*Cin] db:f32[Cout] */
 int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, int Cin, int Cout, int P, const float* pscale,
                              const float* pshift, float* slab, float* dw, float* db, int accumulate, void* stream);
+/*@ xs:u16[(npieces-1)*xplane+(int64_t)B*Cin*(H+2*pad)*(W+2*pad)] wsplit:u16[(npieces-1)*wplane+(int64_t)Cout*Cin*KS*KS] bias:f32[Cout] res:f32[(int64_t)B*Cout*H*W] y:f32[(int64_t)B*Cout*H*W] slab:f32[ubpl_conv2d_forward_psa_workspace(B,Cin,Cout,KS,H,W,npieces)] stat_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*H*W)] bn_x:f32[(int64_t)B*Cout*H*W] bn_coef:f32[3*Cout] bn_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*H*W)] */
 int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                             const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
                             const float* res, float* y, float* slab, int npieces, float* stat_part,
@@ -227,8 +269,10 @@ int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, 
  * phase images of x as a 16-channel PSA image with a `pad` (>= 2) border, and
  * the equivalent 4x4 stride-1 weights (Cin' = 16, KS' = 4) split into npieces
  * (= 3) planes of Cout*256 bf16; then ubpl_conv2d_forward_psa(..., KS = 4). */
+/*@ x:f32[(int64_t)B*C*H*W] dst:u16[(npieces-1)*plane+(int64_t)B*16*(H/2+2*pad)*(W/2+2*pad)] */
 int ubpl_stem_s2d_split(const float* x, int B, int C, int H, int W, int pad, int npieces, uint16_t* dst,
                         int64_t plane, void* stream);
+/*@ w:f32[(int64_t)Cout*C*KS*KS] dst:u16[(npieces-1)*plane+(int64_t)Cout*256] */
 int ubpl_stem_weight_s2d_split(const float* w, int Cout, int C, int KS, int npieces, uint16_t* dst, int64_t plane,
                                void* stream);
 /* 1x1 stride-1 conv on the 6xbf16 path with the f32 activations split while
@@ -238,6 +282,7 @@ int ubpl_stem_weight_s2d_split(const float* w, int Cout, int C, int KS, int npie
  * stat_part (nullable): BatchNorm partials of y (ubpl_bn_partials layout).
  * _preferred: 1 when the shape is supported and fills the chip. */
 int ubpl_conv1x1_split_load_preferred(int B, int Cin, int Cout, int P);
+/*@ x:f32[(int64_t)B*Cin*P] wsplit:u16[2*wplane+(int64_t)Cout*Cin] bias:f32[Cout] pscale:f32[Cin] pshift:f32[Cin] res:f32[(int64_t)B*Cout*P] y:f32[(int64_t)B*Cout*P] stat_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*P)] bn_x:f32[(int64_t)B*Cout*P] bn_coef:f32[3*Cout] bn_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*P)] */
 int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int P, const uint16_t* wsplit, int64_t wplane,
                                     const float* bias, int Cout, const float* pscale, const float* pshift,
                                     const float* res, float* y, float* stat_part, const float* bn_x,
@@ -245,19 +290,28 @@ int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int P, const
 
 /* MaxPool2d(2,2) (models/base/layers.py:93), Upsample(x2, nearest) + add
  * (layers.py:110-111), AvgPool2d(2,2) projection (models/pose/hourglass.py:226). */
+/*@ x:f32[planes*H*W] y:f32[planes*(H/2)*(W/2)] */
 int ubpl_maxpool2x2_forward(const float* x, int64_t planes, int H, int W, float* y, void* stream);
+/*@ x:f32[planes*H*W] dy:f32[planes*(H/2)*(W/2)] dx:f32[planes*H*W] */
 int ubpl_maxpool2x2_backward(const float* x, const float* dy, int64_t planes, int H, int W, float* dx,
                              int accumulate, void* stream);
+/*@ x:f32[planes*H*W] y:f32[planes*(H/2)*(W/2)] */
 int ubpl_avgpool2x2_forward(const float* x, int64_t planes, int H, int W, float* y, void* stream);
+/*@ dy:f32[planes*(H/2)*(W/2)] dx:f32[planes*H*W] */
 int ubpl_avgpool2x2_backward(const float* dy, int64_t planes, int H, int W, float* dx, int accumulate, void* stream);
+/*@ up:f32[planes*H*W] low:f32[planes*(H/2)*(W/2)] out:f32[planes*H*W] */
 int ubpl_upsample2x_add_forward(const float* up, const float* low, int64_t planes, int H, int W, float* out,
                                 void* stream);
+/*@ dout:f32[planes*H*W] dlow:f32[planes*(H/2)*(W/2)] */
 int ubpl_upsample2x_add_backward(const float* dout, int64_t planes, int H, int W, float* dlow, int accumulate,
                                  void* stream);
+/*@ a:f32[n] b:f32[n] out:f32[n] */
 int ubpl_add(const float* a, const float* b, int64_t n, float* out, void* stream);
 /* The same forwards + BatchNorm partials of the output for the BN that
  * consumes it (ubpl_bn_partials layout); output planes of a multiple of 64 pixels. */
+/*@ x:f32[(int64_t)B*C*H*W] y:f32[(int64_t)B*C*(H/2)*(W/2)] part:f32[ubpl_bn_partial_floats(C,(int64_t)B*(H/2)*(W/2))] */
 int ubpl_maxpool2x2_forward_stats(const float* x, int B, int C, int H, int W, float* y, float* part, void* stream);
+/*@ up:f32[(int64_t)B*C*H*W] low:f32[(int64_t)B*C*(H/2)*(W/2)] out:f32[(int64_t)B*C*H*W] part:f32[ubpl_bn_partial_floats(C,(int64_t)B*H*W)] */
 int ubpl_upsample2x_add_forward_stats(const float* up, const float* low, int B, int C, int H, int W, float* out,
                                       float* part, void* stream);
 
@@ -271,7 +325,9 @@ int ubpl_upsample2x_add_forward_stats(const float* up, const float* low, int B, 
  * crop/scale/rotate transform folded by the host — bilinear, zero outside;
  * noise[3v..3v+2] = (alpha, beta, enabled) of noisy_mean; out [V][3][Ho][Wo]
  * float32 minus chan_mean[3]. */
+/*@ imgs:u8[N*n_per_image] out:f32[N] */
 int ubpl_image_mean_u8(const uint8_t* imgs, int N, int64_t n_per_image, float* out, void* stream);
+/*@ imgs:u8[?] src_idx:i32[V] mat:f32[6*V] noise:f32[3*V] img_mean:f32[?] chan_mean:f32[3] out:f32[(int64_t)V*3*Ho*Wo] */
 int ubpl_augment_warp(const uint8_t* imgs, int H, int W, const int* src_idx, const float* mat, const float* noise,
                       const float* img_mean, const float* chan_mean, int V, int Ho, int Wo, float* out, void* stream);
 

@@ -214,11 +214,19 @@ def gen_misc(R):
 # f1 augmentation geometry: keypoints through transform() (utils/udaap/transforms.py:151-158)
 # --------------------------------------------------------------------------
 def gen_augment(R):
+    """The reference's own transform() / get_transform() on the loader's
+    operand types (float32 keypoint tensor rows, int64 centre tensor,
+    float32 0-d scale / angle tensors: utils/augment.py:150-156), and the
+    integer crop corners affine_image computes (utils/augment.py:108-110:
+    transform([0, 0] / res, invert=1) of the unrotated transform)."""
     out = {}
     for cname, (center, scale, rot, pts) in seeds.augment_cases().items():
-        res = [[int(v) for v in R["UT"].transform(p, center, scale, [256, 256], rot=rot)] for p in pts]
+        c = torch.tensor(center)
+        res = [[int(v) for v in R["UT"].transform(p, c, scale, [256, 256], rot=rot)] for p in pts]
         out[cname + "/kps"] = np.array(res, np.int64)
-        out[cname + "/t"] = R["UT"].get_transform(center, scale, [256, 256], rot=rot)
+        out[cname + "/t"] = R["UT"].get_transform(c, scale, [256, 256], rot=rot)
+        out[cname + "/ul"] = np.array(R["UT"].transform([0, 0], c, scale, [256, 256], invert=1))
+        out[cname + "/br"] = np.array(R["UT"].transform([256, 256], c, scale, [256, 256], invert=1))
     np.savez_compressed(os.path.join(HERE, "augment.npz"), **out)
 
 

@@ -190,15 +190,71 @@ def sampler_cases():
 # --------------------------------------------------------------------------
 # f1 augmentation geometry cases (centre, scale, rotation, keypoints)
 # --------------------------------------------------------------------------
+def _f64_transform_ints(pts, center, scale, rot):
+    """transform() at float64 throughout (python-float scale / angle): the
+    arithmetic the f1 fixtures must be able to tell apart from the loader's
+    float32-tensor one (VERDICT r2 weak #1)."""
+    h = 200 * float(scale)
+    t = np.array([[256 / h, 0, 256 * (-center[0] / h + .5)], [0, 256 / h, 256 * (-center[1] / h + .5)], [0, 0, 1.]])
+    if float(rot) != 0:
+        r = -float(rot) * np.pi / 180
+        rm = np.array([[np.cos(r), -np.sin(r), 0], [np.sin(r), np.cos(r), 0], [0, 0, 1.]])
+        tm = np.array([[1, 0, -128.], [0, 1, -128.], [0, 0, 1.]])
+        ti = np.array([[1, 0, 128.], [0, 1, 128.], [0, 0, 1.]])
+        t = ti @ rm @ tm @ t
+    q = np.stack([pts[:, 0].astype(np.float32) - np.float32(1), pts[:, 1].astype(np.float32) - np.float32(1),
+                  np.ones(len(pts), np.float32)]).astype(np.float64)
+    return (t @ q)[:2].T.astype(int) + 1, t
+
+
+def _f32_matrix(center, scale, rot):
+    """get_transform with the loader's float32 tensors (the restatement the
+    product uses, ubpl_amd.augment.get_transform, written out here for the
+    boundary search only; the fixture outputs come from the reference)."""
+    h = 200 * scale
+    t = np.zeros((3, 3))
+    t[0, 0], t[1, 1] = float(256. / h), float(256. / h)
+    t[0, 2], t[1, 2] = float(256 * (-float(center[0]) / h + .5)), float(256 * (-float(center[1]) / h + .5))
+    t[2, 2] = 1
+    if not bool(rot == 0):
+        r = -rot * np.pi / 180
+        sn, cs = float(np.sin(r.numpy())), float(np.cos(r.numpy()))
+        rm = np.array([[cs, -sn, 0], [sn, cs, 0], [0, 0, 1.]])
+        tm = np.array([[1, 0, -128.], [0, 1, -128.], [0, 0, 1.]])
+        ti = np.array([[1, 0, 128.], [0, 1, 128.], [0, 0, 1.]])
+        t = np.dot(ti, np.dot(rm, np.dot(tm, t)))
+    return t
+
+
+def _boundary_points(center, scale, rot, rs, want=3, n=2_000_000):
+    """Keypoints whose transformed coordinate lies so close to an integer that
+    the float64 and the float32-tensor arithmetic truncate it differently."""
+    pts = rs.uniform(1, 255, (n, 2)).astype(np.float32)
+    a64, _ = _f64_transform_ints(pts, center, scale, rot)
+    t32 = _f32_matrix(center, scale, rot)
+    q = np.stack([pts[:, 0] - np.float32(1), pts[:, 1] - np.float32(1), np.ones(n, np.float32)]).astype(np.float64)
+    a32 = (t32 @ q)[:2].T.astype(int) + 1
+    idx = np.nonzero((a64 != a32).any(1))[0][:want]
+    return pts[idx]
+
+
 def augment_cases():
+    """f1 geometry cases as the reference's loader builds them
+    (datasets/dataset_mds.py:60-61, utils/augment.py:18-20): centre ints,
+    scale = f32(256/200) * clamp(1 + 0.25 N(0,1)) and angle = 0 + clamp(30 N(0,1))
+    as float32 0-d tensors, keypoints a float32 tensor — integers, quarter /
+    fractional pixels (image_resize leaves fractions), and points planted
+    where the float64 and float32 arithmetic truncate differently."""
     rs = np.random.RandomState(31)
+    g = torch.Generator().manual_seed(31)
     cases = {}
-    for i in range(6):
-        center = [128, 128] if i % 2 == 0 else [256 - 128, 128]
-        scale = 1.28 * float(np.clip(1 + 0.25 * rs.randn(), 0.75, 1.25))
-        rot = 0.0 if i == 0 else float(np.clip(30 * rs.randn(), -30, 30))
-        pts = rs.randint(1, 256, (9, 2)).astype(np.float32)
-        cases["a%d" % i] = (center, scale, rot, pts)
+    for i in range(8):
+        center = [128, 128] if i % 2 == 0 else [256 - 100, 128]
+        scale = torch.tensor(256 / 200.0) * torch.randn(1, generator=g).mul_(0.25).add_(1).clamp(0.75, 1.25)[0]
+        rot = torch.tensor(0.) + (0. if i == 0 else torch.randn(1, generator=g).mul_(30).clamp(-30, 30)[0])
+        pts = (rs.randint(1, 256, (9, 2)) + rs.choice([0, 0.25, 0.5, 0.371], (9, 2))).astype(np.float32)
+        pts = np.concatenate([pts, _boundary_points(center, scale, rot, rs)])
+        cases["a%d" % i] = (center, scale, rot, torch.from_numpy(pts))
     return cases
 
 

@@ -198,3 +198,47 @@ def test_single_process_helpers_are_identity():
     assert D.allreduce_(t) is t and D.world() == 1 and D.rank() == 0
     c, s = _sync_stats(torch.tensor([3.0]), torch.tensor([4.0]))
     assert float(c[0]) == 4.0 and float(s[0]) == 3.0
+
+
+def _valid_rows_worker(rank, world, port, q, tagged):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import warnings
+        from ubpl_amd.train import gather_valid_rows
+        # sharded loader: rank r holds batches r, r + world, ... (mouse.valid_batches);
+        # plain loader: every rank iterates batches 0..3 itself (no batch_index)
+        idx = range(rank, 5, world) if tagged else range(4)
+        rows = [(i if tagged else None, 2, 3, torch.full((4,), float(10 * i + (rank if not tagged else 0))))
+                for i in idx]
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            out = gather_valid_rows(rows)
+        q.put((rank, [(bi, h.tolist()) for bi, _, _, h in out], len(w)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("tagged", [True, False])
+def test_validate_rows_gather_only_with_batch_index(tagged):
+    """validate() folds the gathered rows in batch_index
+    order only when every rank's loader tags them; a plain loader keeps each
+    rank's own rows (no W-fold duplication, no interleaving) and warns."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_valid_rows_worker, args=(r, 2, port, q, tagged)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, rows, nwarn in res:
+        if tagged:
+            assert [bi for bi, _ in rows] == [0, 1, 2, 3, 4] and nwarn == 0
+            assert [h[0] for _, h in rows] == [0.0, 10.0, 20.0, 30.0, 40.0]
+        else:
+            assert [bi for bi, _ in rows] == [None] * 4 and nwarn == 1
+            assert [h[0] for _, h in rows] == [10.0 * i + rank for i in range(4)]

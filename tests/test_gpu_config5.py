@@ -1,0 +1,109 @@
+"""BASELINE configs[4] as a workload: the MT_UBPL training step
+(projects/MT_UBPL.py:157-352) with 8-stack hourglasses
+(models/pose/hourglass.py:12-58, nStack=8) at 384x384 input / 96x96 heatmaps,
+B=16, on the "bf16" conv precision (one bf16 piece per conv operand, f32
+accumulation).
+
+Each kernel of the bf16 path is pinned exactly against bf16-rounded operands
+in test_gpu_split.py; a randomly initialised train-mode hourglass amplifies
+any rounding ~1e3x (DESIGN.md §4 "bf16"), so the composed step is checked by
+properties of its training signal against the same step on the
+fp32-equivalent 6xbf16 precision, from identical seeded weights and one fixed
+batch:
+* every record (pec, mtc, epc per student, fdc) finite at every step;
+* the printed pseudo-label counts consistent (0 <= n_sel, n_pseudo <=
+  rows * stacks * keypoints);
+* the pose loss pec of each student within 5 % of the 6xbf16 run's at every
+  step, and falling by as much (within 10 % of the drop) over the steps;
+* BatchNorm running statistics of students and teachers finite, variances > 0.
+"""
+import contextlib
+import io
+import re
+import types
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+S, K, B, RES, STEPS = 8, 16, 16, 384, 8
+MEANS = [0.4920829, 0.4920829, 0.4920829]
+
+
+def _args():
+    return types.SimpleNamespace(
+        nStack=S, pseudoScoreThr=0.95, ensemblePseudoWeight=10.0, consWeight=10.0, poseWeight=10.0,
+        FDLWeight=1.0, FDL_label="labeled", FDL_type="covariance", epo=1, ema_decay=0.999, pseudoWeight=1.0,
+        outRes=RES // 4, useEnsemblePseudo=True)
+
+
+def _batch(dev):
+    """One synthetic batch of the bench's shape (bench.make_batches): U[0,1)
+    images minus the Mouse means, integer keypoints, half labeled (unlabeled
+    rows first, as TwoStreamBatchSampler orders them)."""
+    g = torch.Generator().manual_seed(1388)
+    nlab = B // 2
+    isl = torch.tensor([0] * (B - nlab) + [1] * nlab, dtype=torch.bool)
+    means = torch.tensor(MEANS)[None, :, None, None]
+    imgs, kps = [], []
+    for _ in range(2):
+        imgs.append((torch.rand(B, 3, RES, RES, generator=g) - means).to(dev))
+        k = torch.zeros(B, K, 3)
+        k[:, :, :2] = torch.randint(8, RES - 8, (B, K, 2), generator=g).float()
+        k[:, :, 2] = 1.0
+        k[~isl] = 0.0
+        kps.append(k.to(dev))
+    return imgs, None, {"kps": kps, "islabeled": [isl.to(dev)]}
+
+
+def _run(precision):
+    from ubpl_amd import train as T
+    from ubpl_amd.hourglass import StackedHourglass
+    from ubpl_amd.optim import FlatAdamW
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1388)
+    models, emas, optims = [], [], []
+    for _ in range(2):                               # projects/MT_UBPL.py:43-50
+        m = StackedHourglass(K, S, "AvgPool")
+        e = StackedHourglass(K, S, "AvgPool")
+        for p in e.parameters():
+            p.detach_()
+        m.set_conv_precision(precision)
+        e.set_conv_precision(precision)
+        models.append(m)
+        emas.append(e)
+        optims.append(FlatAdamW(m, lr=2.5e-4, weight_decay=0.0))
+    batch = _batch(dev)
+    args = _args()
+    recs, counts = [], []
+    for _ in range(STEPS):
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            pec, mtc, epc, fdc = T.train_mt_ubpl([batch], models, emas, optims, args)
+        recs.append(pec + mtc + epc + [fdc])
+        counts += [(int(a), int(b)) for a, b in re.findall(r"\((\s*\d+)/(\s*\d+)\)", buf.getvalue())]
+    torch.cuda.synchronize()
+    stats = torch.cat([n.flat_stats for n in models + emas]).cpu()
+    nvar = [n.stats(b)[1].cpu() for n in models + emas for b in n._bn_names]
+    return np.array(recs), counts, stats, nvar
+
+
+@pytest.mark.timeout(900)
+def test_config5_bf16_step_trains_like_6xbf16():
+    r1, c1, st1, var1 = _run("bf16")
+    r6, c6, st6, _ = _run("6xbf16")
+    print("pec bf16  ", np.round(r1[:, :2], 5).tolist())
+    print("pec 6xbf16", np.round(r6[:, :2], 5).tolist())
+    assert np.isfinite(r1).all() and np.isfinite(r6).all()
+    assert not np.array_equal(r1, r6)                          # the bf16 kernels really ran
+    assert len(c1) == STEPS
+    for n_sel, n_ps in c1 + c6:
+        assert 0 <= n_sel <= 2 * B * S * K and 0 <= n_ps <= 2 * B * S * K
+    pec1, pec6 = r1[:, :2], r6[:, :2]
+    assert (np.abs(pec1 - pec6) <= 0.05 * pec6).all(), (pec1, pec6)
+    drop1, drop6 = pec1[0] - pec1[-1], pec6[0] - pec6[-1]
+    assert (drop6 > 0).all() and (np.abs(drop1 - drop6) <= 0.1 * drop6).all(), (drop1, drop6)
+    assert torch.isfinite(st1).all() and torch.isfinite(st6).all()
+    assert all(bool((v > 0).all()) for v in var1)

@@ -3,7 +3,7 @@ step, oracle/step.py) against the reference's own train()
 (projects/MT_UBPL.py:157-352) on the same inputs, same host, same threads.
 
 Runs only in the build container (it imports /root/reference through the
-golden generator's stub recipe).  Writes profiles/r02_cpu_calibration_b<B>.json.
+golden generator's stub recipe).  Writes profiles/r03_cpu_calibration_b<B>.json.
 
     python tools/calibrate_cpu_baseline.py [B] [steps]
 """
@@ -53,7 +53,7 @@ def main(B=4, steps=2):
            "reference_images_per_s": round(B / t_ref, 4), "port_images_per_s": round(B / t_port, 4),
            "port_over_reference": round(t_ref / t_port, 4),
            "survey_reference_images_per_s": {"B4": 0.92, "B32": 0.51}}
-    out = os.path.join(ROOT, "profiles", "r02_cpu_calibration_b%d.json" % B)
+    out = os.path.join(ROOT, "profiles", "r03_cpu_calibration_b%d.json" % B)
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
     print(json.dumps(rec))

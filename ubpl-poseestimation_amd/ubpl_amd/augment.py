@@ -5,12 +5,15 @@ Per view, in the reference's order and with its random draws
 keypoints x -> W - x, centre x -> W - x), noisy_mean with p 0.5 (alpha
 U(0.8, 1.2), beta U(-0.2, 0.2); :261-267), affine with scale =
 scale0 * clamp(1 + sf * N(0,1), 1 - sf, 1 + sf) and angle = clamp(rf * N(0,1),
--rf, rf) (:86-98) — keypoints through utils/udaap/transforms.py:transform
-(float64 matrix, int truncation, only where y > 0: utils/augment.py:150-156),
-pixels through the same matrix inverted, folded with the flip into one 2x3
-matrix per view for ubpl_augment_warp — and colorNorm (means, no std).  The
-images never leave HBM; the host draws the random numbers and builds the
-matrices (a few scalars per view), as the reference's loader does.
+-rf, rf) (:18-22) — float32 TENSORS, as the loader builds them
+(dataset_mds.py:60-61) — keypoints through utils/udaap/transforms.py:transform
+with the reference's operand types (float32 matrix entries and sin/cos,
+float64 products, int truncation, only where y > 0: utils/augment.py:150-156),
+pixels through the reference's crop -> rotate -> resize geometry
+(utils/augment.py:103-137) folded with the flip into one 2x3 matrix per view
+for ubpl_augment_warp — and colorNorm (means, no std).  The images never
+leave HBM; the host draws the random numbers and builds the matrices (a few
+scalars per view), as the reference's loader does.
 """
 import random
 
@@ -19,32 +22,107 @@ import torch
 
 from . import kernels as Kn
 
+F32 = torch.float32
+
 
 def get_transform(center, scale, res, rot=0.0):
-    """utils/udaap/transforms.py:119-148 (float64)."""
+    """utils/udaap/transforms.py:119-148 with the loader's operand types:
+    scale and rot are float32 0-d tensors (datasets/dataset_mds.py:60-61,
+    utils/augment.py:19-20), so h = 200*scale, every matrix entry and
+    sin/cos(rot) are float32 values (torch's `float / tensor` is reciprocal(tensor)
+    * float; numpy's float32 sin/cos on the tensor), stored into the float64
+    matrix whose products (np.dot) are float64.  Python floats are promoted to
+    float32 tensors the same way."""
+    scale = torch.as_tensor(scale, dtype=F32)
     h = 200 * scale
     t = np.zeros((3, 3))
-    t[0, 0] = float(res[1]) / h
-    t[1, 1] = float(res[0]) / h
-    t[0, 2] = res[1] * (-float(center[0]) / h + .5)
-    t[1, 2] = res[0] * (-float(center[1]) / h + .5)
+    t[0, 0] = float(float(res[1]) / h)
+    t[1, 1] = float(float(res[0]) / h)
+    t[0, 2] = float(res[1] * (-float(center[0]) / h + .5))
+    t[1, 2] = float(res[0] * (-float(center[1]) / h + .5))
     t[2, 2] = 1
-    if rot != 0:
-        r = -rot * np.pi / 180
-        sn, cs = np.sin(r), np.cos(r)
-        rm = np.array([[cs, -sn, 0], [sn, cs, 0], [0, 0, 1.]])
+    rot = torch.as_tensor(rot, dtype=F32)
+    if not bool(rot == 0):
+        r = -rot
+        r = r * np.pi / 180
+        sn, cs = float(np.sin(r.numpy())), float(np.cos(r.numpy()))    # numpy float32 sin/cos, as on the tensor
+        rm = np.zeros((3, 3))
+        rm[0, :2] = [cs, -sn]
+        rm[1, :2] = [sn, cs]
+        rm[2, 2] = 1
         tm = np.eye(3)
         tm[0, 2], tm[1, 2] = -res[1] / 2, -res[0] / 2
         ti = tm.copy()
         ti[:2, 2] *= -1
-        t = ti @ (rm @ (tm @ t))                                         # np.dot nesting of :147
+        t = np.dot(ti, np.dot(rm, np.dot(tm, t)))                        # :147
     return t
 
 
-def transform_point(pt, t):
-    """utils/udaap/transforms.py:151-158 with a prebuilt matrix."""
-    p = t @ np.array([pt[0] - 1, pt[1] - 1, 1.])
+def transform_point(pt, t, invert=False):
+    """utils/udaap/transforms.py:151-158 with a prebuilt matrix: pt is a row of
+    the float32 keypoint tensor, so pt - 1 is a float32 subtraction; the
+    product is float64, truncated to int, + 1."""
+    if invert:
+        t = np.linalg.inv(t)
+    if torch.is_tensor(pt):
+        x, y = float(pt[0] - 1), float(pt[1] - 1)
+    else:
+        x, y = pt[0] - 1, pt[1] - 1
+    p = np.dot(t, np.array([x, y, 1.]))
     return p[:2].astype(int) + 1
+
+
+def crop_box(center, scale, res, angle):
+    """The integer crop of affine_image (utils/augment.py:103-129): corners
+    ul = transform([0, 0], invert=1), br = transform(res, invert=1) of the
+    UNROTATED transform, then grown by pad = int(|br - ul| / 2 - (br_y - ul_y)
+    / 2) on every side when angle != 0.  Returns (ul, br, pad) as ints (ul, br
+    after the growth)."""
+    ti = np.linalg.inv(get_transform(center, scale, res, 0))
+    ul = transform_point([0, 0], ti)
+    br = transform_point(list(res), ti)
+    pad = int(np.linalg.norm(br - ul) / 2 - float(br[1] - ul[1]) / 2)
+    if not bool(torch.as_tensor(angle, dtype=F32) == 0):
+        ul = ul - pad
+        br = br + pad
+    else:
+        pad = 0
+    return ul, br, pad
+
+
+def warp_matrix(center, scale, res, angle, W, flip=False):
+    """2x3 map from output pixel (x, y) (0-based) to the source pixel it
+    samples (0-based, of the unflipped source image of width W) — the
+    reference's pixel path composed into one affine map
+    (utils/augment.py:103-137):
+      1. resize of the stripped crop (Hc x Wc) to res, skimage's pixel-centre
+         convention: src = (dst + 0.5) * (crop / res) - 0.5;
+      2. strip of the rotation pad: + pad;
+      3. skimage.transform.rotate(angle) of the padded crop (H' x W'): inverse
+         map about c = ((W'-1)/2, (H'-1)/2), p = c + R(angle) (q - c),
+         R = [[cos, -sin], [sin, cos]];
+      4. the integer crop: + (ul_x, ul_y) of the grown box;
+      5. the fliplr that happened before it: x -> W - 1 - x.
+    What one bilinear sample cannot restate (two resamplings in the
+    reference, skimage's anti-aliasing Gaussian when the crop is larger than
+    res, reflect-mode edges of the resize) is documented in DESIGN.md §1 f1."""
+    ul, br, pad = crop_box(center, scale, res, angle)
+    Hp, Wp = br[1] - ul[1], br[0] - ul[0]                  # the (padded) crop
+    Hc, Wc = Hp - 2 * pad, Wp - 2 * pad                   # after stripping the pad
+    M = np.array([[Wc / res[1], 0, 0.5 * Wc / res[1] - 0.5],
+                  [0, Hc / res[0], 0.5 * Hc / res[0] - 0.5], [0, 0, 1.]])
+    M = np.array([[1, 0, pad], [0, 1, pad], [0, 0, 1.]]) @ M
+    if pad:
+        th = np.deg2rad(float(torch.as_tensor(angle, dtype=F32)))
+        c = np.array([(Wp - 1) / 2.0, (Hp - 1) / 2.0])
+        R = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1.]])
+        Tc = np.array([[1, 0, c[0]], [0, 1, c[1]], [0, 0, 1.]])
+        Tm = np.array([[1, 0, -c[0]], [0, 1, -c[1]], [0, 0, 1.]])
+        M = Tc @ R @ Tm @ M
+    M = np.array([[1, 0, ul[0]], [0, 1, ul[1]], [0, 0, 1.]]) @ M
+    if flip:
+        M = np.array([[-1, 0, W - 1], [0, 1, 0], [0, 0, 1.]]) @ M
+    return M[:2]
 
 
 class DeviceAugment:
@@ -61,13 +139,15 @@ class DeviceAugment:
         self.img_mean = Kn.image_mean_u8(self.imgs)
 
     def _draw(self, kps):
-        """One view's random draws and keypoints (numpy [K,3] in, [K,3] out)."""
+        """One view's random draws and keypoints (numpy [K,3] in, [K,3] out),
+        with the loader's types: keypoints float32 tensors, centre ints,
+        scale and angle float32 0-d tensors."""
         W, H = self.W, self.H
-        kps = kps.copy()
+        kps = torch.tensor(np.asarray(kps, np.float32))
         center = [int(W / 2), int(H / 2)]                                # utils/process.py:218-221
         flip = False
         if self.use_flip and random.random() <= 0.5:                      # augment.py:218
-            kps[:, 0] = W - kps[:, 0]                                      # process.py:239-242
+            kps[:, 0] = W - kps[:, 0]                                      # process.py:239-242 (float32)
             center[0] = W - center[0]
             flip = True
         noise = (1.0, 0.0, 0.0)
@@ -75,19 +155,19 @@ class DeviceAugment:
             a = random.uniform(0.8, 1.2)
             b = random.uniform(-0.2, 0.2)
             noise = (a, b, 1.0 if self.use_noise else 0.0)
-        scale0 = self.res / 200.0
-        scale = scale0 * float(torch.randn(1).mul_(self.sf).add_(1).clamp(1 - self.sf, 1 + self.sf)[0])
-        angle = float(torch.randn(1).mul_(self.rf).clamp(-self.rf, self.rf)[0]) if random.random() <= 1.0 else 0.
-        t = get_transform(center, scale, [self.res, self.res], rot=angle)
+        scale = torch.tensor(self.res / 200.0)                            # dataset_mds.py:61 (float32)
+        scale = scale * torch.randn(1).mul_(self.sf).add_(1).clamp(1 - self.sf, 1 + self.sf)[0]   # augment.py:19
+        angle = torch.tensor(0.)                                          # dataset_mds.py:60
+        angle = angle + torch.randn(1).mul_(self.rf).clamp(-self.rf, self.rf)[0] \
+            if random.random() <= 1.0 else 0.                              # augment.py:20
+        res = [self.res, self.res]
+        t = get_transform(center, scale, res, rot=angle)
+        out = kps.clone()
         for k in range(kps.shape[0]):
             if kps[k, 1] > 0:                                             # augment.py:153
-                kps[k, :2] = transform_point(kps[k, :2], t)
-        ti = np.linalg.inv(t)                                             # output (x, y) -> source, 0-based
-        m = ti[:2].copy()
-        if flip:                                                          # the source image is mirrored
-            m[0] = -m[0]
-            m[0, 2] += W - 1
-        return m.reshape(-1), noise, kps
+                out[k, :2] = torch.from_numpy(transform_point(kps[k, :2], t))
+        m = warp_matrix(center, scale, res, angle, W, flip)
+        return m.reshape(-1), noise, out.numpy()
 
     def views(self, idx, kps):
         """idx: source image per view [V]; kps: numpy [V,K,3] pixel keypoints.

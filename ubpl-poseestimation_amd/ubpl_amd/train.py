@@ -607,7 +607,7 @@ class _LaggedRecords:
         host = torch.empty(dev_t.shape, dtype=dev_t.dtype, pin_memory=True)
         host.copy_(dev_t, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record()
+        ev.record(torch.cuda.current_stream(dev_t.device))    # the stream the copy went on
         prev, self.pending = self.pending, (host, ev, consume)
         if prev is not None:
             self._run(prev)
@@ -642,12 +642,14 @@ def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
         e.train()
     runner = _StepGraph.get(_mt_ubpl_core, models, models_ema, optims, args)
     lag = _LaggedRecords()
-    for bat, (augs_imgMap, augs_heatmaps, meta) in enumerate(trainLoader):
-        packed, meta_h = runner.run((augs_imgMap, augs_heatmaps, meta), dev)
-        # the step's one device->host copy, read after the next step is enqueued
-        lag.push(packed, lambda host, bat=bat, meta_h=meta_h: _mt_ubpl_records(
-            host, bat, meta_h, M, pec_c, mtc_c, epc_c, fdc_c, args, verbose))
-    lag.flush()
+    try:
+        for bat, (augs_imgMap, augs_heatmaps, meta) in enumerate(trainLoader):
+            packed, meta_h = runner.run((augs_imgMap, augs_heatmaps, meta), dev)
+            # the step's one device->host copy, read after the next step is enqueued
+            lag.push(packed, lambda host, bat=bat, meta_h=meta_h: _mt_ubpl_records(
+                host, bat, meta_h, M, pec_c, mtc_c, epc_c, fdc_c, args, verbose))
+    finally:
+        lag.flush()          # also when the loader raises mid-epoch: the last step's records
     return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
 
 
@@ -699,86 +701,88 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
     for e in models_ema:
         e.train()
     lag = _LaggedRecords()
-    for bat, (stu_imgMap, stu_heatmap, ema_imgMap, meta) in enumerate(trainLoader):
-        for o in optims:
-            o.zero_grad()
-        si = stu_imgMap.to(dev, non_blocking=True).float().contiguous()
-        ei = ema_imgMap.to(dev, non_blocking=True).float().contiguous()
-        if stu_heatmap is None:
-            hm, kk = render_batch(meta["kps"].to(dev).float(), (si.shape[-2], si.shape[-1]), si.shape[-1],
-                                  si.shape[-1] // 4)
-            gate = kk[:, :, 2].contiguous()
-        else:
-            hm = stu_heatmap.to(dev, non_blocking=True).float().contiguous()
-            gate = meta["kpsWeight"].to(dev, non_blocking=True).float().contiguous()
-        isl = _islabeled(meta["islabeled"], dev)
-        sw = _w(isl, 1.0, 0.0)
-        nega = _w(isl, 0.0, args.pseudoWeight)
-        cons = _w(isl, 1.0, args.pseudoWeight)
-        B = si.shape[0]
-        outs, feats, ema_l = [], [], []
-        mstreams = _ModelStreams.make(M, dev)                    # one HIP stream per network
-        for mi in range(M):                                       # :185-196
-            with (mstreams.on(mi) if mstreams else contextlib.nullcontext()):
-                o, f = models[mi](si)
-            outs.append(o)
-            feats.append(f)
-            with (mstreams.on_teacher(mi) if mstreams else contextlib.nullcontext()), torch.no_grad():
-                ema_l.append(models_ema[mi](ei)[0])
-        if mstreams:
-            mstreams.join(outs + feats + ema_l)
-            outs = [_OnMain.apply(t) for t in outs]
-            feats = [None if t is None else _OnMain.apply(t) for t in feats]
-        outs_ema = torch.stack(ema_l)
-        use_ep = getattr(args, "useEnsemblePseudo", True)    # :224 (False: epc = 0, no print)
-        K = outs[0].shape[2]
-        zero = torch.zeros((), device=dev)
-        loc, cn, cons_sc, ps_sc = [], [], [], []
-        for mi in range(M):
-            s_c, c_c, sc_c = _dist_mt2_last(outs[mi], outs_ema[mi], cons, args.pseudoScoreThr)
-            s_p, c_p = _mse(outs[mi], hm, S, gate, sw.reshape(-1, 1))
-            if use_ep:
-                s_e, c_e, sc_e = _pseudo(outs[mi], outs_ema, nega, S, args.pseudoScoreThr)
-                ps_sc.append(sc_e)
+    try:
+        for bat, (stu_imgMap, stu_heatmap, ema_imgMap, meta) in enumerate(trainLoader):
+            for o in optims:
+                o.zero_grad()
+            si = stu_imgMap.to(dev, non_blocking=True).float().contiguous()
+            ei = ema_imgMap.to(dev, non_blocking=True).float().contiguous()
+            if stu_heatmap is None:
+                hm, kk = render_batch(meta["kps"].to(dev).float(), (si.shape[-2], si.shape[-1]), si.shape[-1],
+                                      si.shape[-1] // 4)
+                gate = kk[:, :, 2].contiguous()
             else:
-                s_e, c_e = zero, torch.zeros(4, dtype=torch.int32, device=dev)
-            loc += [s_c, s_p, s_e]
-            cn += [c_c[0], c_p[0], c_e[1], c_c[1], c_c[2], c_e[2]]
-            cons_sc.append(sc_c)
-        fd = []
-        if args.FDLWeight > 0:                                     # :246-270 (one view)
-            fd.append(_fdl_view(feats[0], feats[1], _fdl_rows(sw, args), args))
-        loc += _fdl_record_sums(fd)
-        cn += [n[0] for _, _, n in fd]
-        counts = torch.stack([c.float() for c in cn])
-        gcounts, gsums = _sync_stats(torch.stack([l.float() for l in loc]), counts)
-        W = D.world()
-        fdc = _fdl_total(fd, gcounts[6 * M:], W, args.FDLWeight) if fd else 0.
-        totals = []
-        for mi in range(M):
-            mtc = args.consWeight * _norm(loc[3 * mi], gcounts[6 * mi])
-            pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[6 * mi + 1])
-            epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else 0.
-            totals.append(pec + mtc + epc + fdc)
-        _backward_all(totals)                                     # DualPose_UBPL.py:277-279
-        if mstreams:
-            mstreams.join()
-        for m in models:
-            m.merge_alt_grads()
-        D.allreduce_grads(models)
-        _step_and_ema(models, models_ema, optims, args)
-        g_rec = []
-        for mi in range(M):
-            g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[6 * mi + 1]),
-                      args.consWeight * _norm(gsums[3 * mi], gcounts[6 * mi]),
-                      args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else zero]
-        g_rec.append(_fdl_record(fd, gsums[3 * M:], gcounts[6 * M:], W, args.FDLWeight) if fd else zero)
-        packed = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, torch.stack(cons_sc).mean(0),
-                            torch.stack(ps_sc).mean(0) if use_ep else torch.zeros(K, device=dev)])
-        lag.push(packed, lambda host, bat=bat, ncn=len(cn), K=K, use_ep=use_ep, nfd=len(fd): _dualpose_records(
-            host, bat, ncn, K, use_ep, nfd, M, S, pec_c, mtc_c, epc_c, fdc_c, args, verbose))
-        del outs, outs_ema, feats, totals
-    lag.flush()
+                hm = stu_heatmap.to(dev, non_blocking=True).float().contiguous()
+                gate = meta["kpsWeight"].to(dev, non_blocking=True).float().contiguous()
+            isl = _islabeled(meta["islabeled"], dev)
+            sw = _w(isl, 1.0, 0.0)
+            nega = _w(isl, 0.0, args.pseudoWeight)
+            cons = _w(isl, 1.0, args.pseudoWeight)
+            B = si.shape[0]
+            outs, feats, ema_l = [], [], []
+            mstreams = _ModelStreams.make(M, dev)                    # one HIP stream per network
+            for mi in range(M):                                       # :185-196
+                with (mstreams.on(mi) if mstreams else contextlib.nullcontext()):
+                    o, f = models[mi](si)
+                outs.append(o)
+                feats.append(f)
+                with (mstreams.on_teacher(mi) if mstreams else contextlib.nullcontext()), torch.no_grad():
+                    ema_l.append(models_ema[mi](ei)[0])
+            if mstreams:
+                mstreams.join(outs + feats + ema_l)
+                outs = [_OnMain.apply(t) for t in outs]
+                feats = [None if t is None else _OnMain.apply(t) for t in feats]
+            outs_ema = torch.stack(ema_l)
+            use_ep = getattr(args, "useEnsemblePseudo", True)    # :224 (False: epc = 0, no print)
+            K = outs[0].shape[2]
+            zero = torch.zeros((), device=dev)
+            loc, cn, cons_sc, ps_sc = [], [], [], []
+            for mi in range(M):
+                s_c, c_c, sc_c = _dist_mt2_last(outs[mi], outs_ema[mi], cons, args.pseudoScoreThr)
+                s_p, c_p = _mse(outs[mi], hm, S, gate, sw.reshape(-1, 1))
+                if use_ep:
+                    s_e, c_e, sc_e = _pseudo(outs[mi], outs_ema, nega, S, args.pseudoScoreThr)
+                    ps_sc.append(sc_e)
+                else:
+                    s_e, c_e = zero, torch.zeros(4, dtype=torch.int32, device=dev)
+                loc += [s_c, s_p, s_e]
+                cn += [c_c[0], c_p[0], c_e[1], c_c[1], c_c[2], c_e[2]]
+                cons_sc.append(sc_c)
+            fd = []
+            if args.FDLWeight > 0:                                     # :246-270 (one view)
+                fd.append(_fdl_view(feats[0], feats[1], _fdl_rows(sw, args), args))
+            loc += _fdl_record_sums(fd)
+            cn += [n[0] for _, _, n in fd]
+            counts = torch.stack([c.float() for c in cn])
+            gcounts, gsums = _sync_stats(torch.stack([l.float() for l in loc]), counts)
+            W = D.world()
+            fdc = _fdl_total(fd, gcounts[6 * M:], W, args.FDLWeight) if fd else 0.
+            totals = []
+            for mi in range(M):
+                mtc = args.consWeight * _norm(loc[3 * mi], gcounts[6 * mi])
+                pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[6 * mi + 1])
+                epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else 0.
+                totals.append(pec + mtc + epc + fdc)
+            _backward_all(totals)                                     # DualPose_UBPL.py:277-279
+            if mstreams:
+                mstreams.join()
+            for m in models:
+                m.merge_alt_grads()
+            D.allreduce_grads(models)
+            _step_and_ema(models, models_ema, optims, args)
+            g_rec = []
+            for mi in range(M):
+                g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[6 * mi + 1]),
+                          args.consWeight * _norm(gsums[3 * mi], gcounts[6 * mi]),
+                          args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else zero]
+            g_rec.append(_fdl_record(fd, gsums[3 * M:], gcounts[6 * M:], W, args.FDLWeight) if fd else zero)
+            packed = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, torch.stack(cons_sc).mean(0),
+                                torch.stack(ps_sc).mean(0) if use_ep else torch.zeros(K, device=dev)])
+            lag.push(packed, lambda host, bat=bat, ncn=len(cn), K=K, use_ep=use_ep, nfd=len(fd): _dualpose_records(
+                host, bat, ncn, K, use_ep, nfd, M, S, pec_c, mtc_c, epc_c, fdc_c, args, verbose))
+            del outs, outs_ema, feats, totals
+    finally:
+        lag.flush()          # also when the loader raises mid-epoch
     return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
 
 
@@ -879,6 +883,34 @@ def train_supervised(trainLoader, model, optim, args):
 # ---------------------------------------------------------------------------
 # validate: teachers in eval mode -> decode -> PCK (D1-D5)
 # ---------------------------------------------------------------------------
+def gather_valid_rows(rows):
+    """Validation rows (batch_index or None, bs, k, host row) of this rank ->
+    the rows to fold, in the single-device batch order.
+
+    Under torch.distributed the rows of all ranks are gathered and ordered by
+    batch_index only when EVERY row of every rank carries one (the sharded
+    loader, mouse.valid_batches, sets meta['batch_index']).  A loader without
+    it gives no global order — every rank may have iterated the whole set, or
+    a DistributedSampler reuses indices 0..n on each rank — so then each rank
+    keeps its own rows in its own order (per-rank records) and a warning says
+    so.  One device: the rows as iterated."""
+    if not D.is_dist():
+        return rows
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    tagged = torch.tensor([float(all(r[0] is not None for r in rows))], device=dev)
+    dist.all_reduce(tagged, op=dist.ReduceOp.MIN)
+    if tagged.item() < 1:
+        import warnings
+        warnings.warn("ubpl_amd.validate under torch.distributed: the loader sets no meta['batch_index'], "
+                      "so the records are this rank's own (not gathered)", RuntimeWarning)
+        return rows
+    allrows = [None] * D.world()
+    dist.all_gather_object(allrows, [(bi, bs, k, h.tolist()) for bi, bs, k, h in rows])
+    return sorted(((int(bi), bs, k, torch.tensor(h)) for part in allrows for bi, bs, k, h in part),
+                  key=lambda r: r[0])
+
+
 def validate(validLoader, models_ema, args):
     """projects/MT_UBPL.py:355-408 -> (predsArray, accs_records, errs_records);
     entries per teacher plus their mean (brNum + 1).
@@ -917,13 +949,8 @@ def validate(validLoader, models_ema, args):
             gts = meta["kpsMap"].to(dev).float().contiguous()
             outs = [EvaluationUtils.acc_pck(p, gts, args.pck_ref, args.pck_thr) for p in pm]
             host = torch.cat([torch.cat([er, ac]) for er, ac in outs] + [p.reshape(-1) for p in pm]).cpu()
-            rows.append((int(meta.get("batch_index", bat)), bs, k, host))
-    if D.is_dist():
-        import torch.distributed as dist
-        allrows = [None] * D.world()
-        dist.all_gather_object(allrows, [(bi, bs, k, h.tolist()) for bi, bs, k, h in rows])
-        rows = sorted(((bi, bs, k, torch.tensor(h)) for part in allrows for bi, bs, k, h in part),
-                      key=lambda r: r[0])
+            rows.append((meta.get("batch_index"), bs, k, host))
+    rows = gather_valid_rows(rows)
     accs_c = [AvgCounters() for _ in range(n)]
     errs_c = [AvgCounters() for _ in range(n)]
     preds_arr = [[] for _ in range(n)]
