@@ -85,7 +85,23 @@ def make_batches(n, B, K, dev, seed, res=256, dualpose=False):
     return out
 
 
-ROOF_SHAPE = (128, 128, 3, 64, 64)   # Cin, Cout, KS, H, W of the roofline kernel's launches
+ROOF_SHAPE = (128, 128, 3, 64, 64)   # Cin, Cout, KS, H, W of the roofline kernel's launches (headline)
+# per config: (Cin, Cout, KS, H, W) of the dominant conv_psa_kernel launches, pieces per operand, peak,
+# description.  HG8 at 384^2 runs its top hourglass level on 96x96 planes.
+ROOF = {
+    "mt_ubpl": ((128, 128, 3, 64, 64), 3, SPLIT6_PEAK_TFLOPS,
+                "conv_psa_kernel<128, 3, 3, 256, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; 6xbf16 "
+                "split-f32 MFMA; f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
+    "dualpose_hg4": ((128, 128, 3, 64, 64), 3, SPLIT6_PEAK_TFLOPS,
+                     "conv_psa_kernel<128, 3, 3, 256, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
+                     "6xbf16; f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
+    "mt_ubpl_hg8_384": ((128, 128, 3, 96, 96), 3, SPLIT6_PEAK_TFLOPS,
+                        "conv_psa_kernel (3x3 conv, 128->128 ch, 96x96 planes, fwd + dgrad; 6xbf16; "
+                        "f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
+    "mt_ubpl_hg8_384_bf16": ((128, 128, 3, 96, 96), 1, 2500.0,
+                             "conv_psa_kernel (3x3 conv, 128->128 ch, 96x96 planes, fwd + dgrad; bf16 operands, "
+                             "f32 accumulation; peak = bf16 dense MFMA)"),
+}
 
 
 class PsaLaunches:
@@ -96,8 +112,8 @@ class PsaLaunches:
     256, 2> (rocprofv3 names it so), with no split-K slab — and keeps every
     tensor those pointers reference alive, so the launches can be replayed."""
 
-    def __init__(self, Kn, lib):
-        self.Kn, self.lib = Kn, lib
+    def __init__(self, Kn, lib, shape=ROOF_SHAPE):
+        self.Kn, self.lib, self.shape = Kn, lib, tuple(shape)
         self.calls, self.keep = [], []
 
     def __enter__(self):
@@ -112,7 +128,7 @@ class PsaLaunches:
 
         def psa(xs, ws, bias, res=None, out=None, stat_part=None, bwd=None):
             Cout, T, _ = ws.shape
-            rec._want = (xs.C, Cout, int(round(T ** 0.5)), xs.H, xs.W) == ROOF_SHAPE
+            rec._want = (xs.C, Cout, int(round(T ** 0.5)), xs.H, xs.W) == rec.shape
             y = orig_psa(xs, ws, bias, res, out, stat_part, bwd)
             if rec._want:
                 rec.keep.append((xs, ws, bias, res, y, stat_part, bwd))
@@ -153,24 +169,27 @@ class PsaLaunches:
         return s.elapsed_time(e) / (reps * len(calls)), len(calls)
 
 
-def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step):
-    """The dominant kernel: conv_psa_kernel<128,3,3,256,2> (3x3 conv on the
-    6xbf16 split path at the 64x64 planes, forward + data gradient; the
-    largest single entry of the rocprofv3 kernel summary, profiles/r02_*).
-    achieved = algorithmic f32-equivalent FLOP per launch (2*B*Cout*Cin*9*H*W)
-    / its average standalone launch duration (HIP events around replayed
-    launches, see PsaLaunches.time), vs 2.5 PF bf16 dense / 6 piece products."""
+def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config="mt_ubpl", train=None):
+    """The dominant kernel: conv_psa_kernel at the config's largest 3x3 planes
+    (headline: conv_psa_kernel<128,3,3,256,2>, the 3x3 conv on the 6xbf16 split
+    path at the 64x64 planes, forward + data gradient; the largest single entry
+    of the rocprofv3 kernel summary, profiles/r0*_summary).
+    achieved = algorithmic FLOP per launch (2*B*Cout*Cin*9*H*W; f32-equivalent
+    on the split path) / its average standalone launch duration (HIP events
+    around replayed launches, see PsaLaunches.time), vs the config's peak
+    (6xbf16: 2.5 PF bf16 dense / 6 piece products; bf16: 2.5 PF)."""
+    shape, npieces, peak, desc = ROOF[config]
     os.environ["UBPL_MODEL_STREAMS"] = "0"
     try:
-        with PsaLaunches(Kn, lib) as rec, T._StepGraph.eager():
-            T.train_mt_ubpl([batch], models, emas, optims, args, verbose=False)
+        with PsaLaunches(Kn, lib, shape) as rec, T._StepGraph.eager():
+            (train or T.train_mt_ubpl)([batch], models, emas, optims, args, verbose=False)
         torch.cuda.synchronize()
         avg_ms, n = rec.time()
     finally:
         del os.environ["UBPL_MODEL_STREAMS"]
     if avg_ms is None:
         return None
-    Cin, Cout, KS, H, W = ROOF_SHAPE
+    Cin, Cout, KS, H, W = shape
     B = args.batch
     flops = 2 * B * Cout * Cin * KS * KS * H * W
     achieved = flops / (avg_ms * 1e-3) / 1e12
@@ -181,12 +200,11 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step):
     if not consistent:
         print("bench: roofline kernel replays sum to %.2f ms > %.2f ms/step" % (per_step_ms, ms_per_step),
               file=sys.stderr)
-    pmc = pmc_traffic("psa")
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(SPLIT6_PEAK_TFLOPS, 2),
-            "unit": "TFLOP/s", "frac": round(achieved / SPLIT6_PEAK_TFLOPS, 4),
+    pmc = pmc_traffic("psa") if config == "mt_ubpl" else None
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2),
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": (pmc or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc,
-            "kernel": "conv_psa_kernel<128, 3, 3, 256, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
-                      "6xbf16 split-f32 MFMA; f32-equivalent FLOP/s, peak = bf16 dense / 6)",
+            "kernel": desc, "pieces": npieces,
             "flops_per_launch": flops, "launches_per_step": n, "avg_launch_us": round(avg_ms * 1e3, 2),
             "kernel_ms_per_step": round(per_step_ms, 3), "fits_in_step": consistent,
             "timing": "HIP events around back-to-back replays of the step's launches of this kernel "
@@ -355,7 +373,7 @@ def main():
     # roofline kernel: its launches from one more (eager, untimed) step, replayed
     # back to back between HIP events (standalone duration; see roofline())
     args.batch = B
-    roof = roofline(Kn, _lib, T, models, emas, optims, args, timed[0], dt / a.steps * 1e3) if headline else None
+    roof = roofline(Kn, _lib, T, models, emas, optims, args, timed[0], dt / a.steps * 1e3, a.config, train)
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

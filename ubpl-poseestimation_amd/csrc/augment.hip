@@ -8,15 +8,18 @@
 // one launch writes a whole batch of augmented views as float32 NCHW.
 //
 // Geometry: output pixel (x, y) samples the flipped, noise-adjusted source at
-// T^-1 (x, y, 1), T = get_transform(center, scale, res, rot)
-// (utils/udaap/transforms.py:119-148) — the SAME map the keypoints go through
-// (utils/augment.py:150-156, host side), so heatmaps and pixels agree.  The
-// host folds the flip (source column W-1-x) and T^-1 into one 2x3 matrix per
-// view.  Bilinear sampling (skimage order 1) with zero outside the image
-// (skimage's constant 0 padding).  Not reproduced: skimage.resize's Gaussian
-// anti-aliasing when a view is scaled down (<= 25 % here) and its integer-
-// rounded crop box — skimage is not in this image, so this stage has
-// statistical, not bitwise, parity.
+// M (x, y, 1), M = the reference's pixel chain composed on the host
+// (augment.warp_matrix): skimage.resize's pixel centres of the stripped crop,
+// the rotation pad, skimage.transform.rotate's inverse map about the padded
+// crop's centre, the integer crop corners transform([0,0] / res, invert=1)
+// (utils/augment.py:103-137), and the flip (source column W-1-x).  The
+// keypoints go through transform() with the same float32 operands on the host
+// (utils/augment.py:150-156).  Bilinear sampling (skimage order 1) with zero
+// outside the image (skimage's constant 0 padding).  Not reproduced: the
+// reference resamples twice (rotate, then resize) where this samples once,
+// skimage.resize's Gaussian anti-aliasing when a view is scaled down (<= 25 %
+// here) and its reflect-mode edges — skimage is not in this image, so the
+// pixels have statistical, not bitwise, parity.
 //
 // noisy_mean: v' = clamp(alpha * (v - mu) + mu + beta, 0, 1) on the [0,1]
 // source pixels with mu the image mean over all channels and pixels

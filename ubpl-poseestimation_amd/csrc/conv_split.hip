@@ -28,7 +28,15 @@ typedef short short8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
+#ifndef UBPL_PSA_PP
+#define UBPL_PSA_PP 1
+#endif
+#ifndef UBPL_SOL_PP
+#define UBPL_SOL_PP 0
+#endif
+
 constexpr int NT = 256;
+constexpr int SOL_PRO_K = 512;   // conv1x1_sol_kernel: largest input channel count with a prologue
 constexpr int BK = 32;
 constexpr int BN = 128;
 
@@ -43,6 +51,21 @@ __device__ __forceinline__ void mfma_split(floatx16& acc, const bf16x8 (&a)[NP],
     for (int d = NP - 1; d >= 0; --d)
 #pragma unroll
         for (int pa = d; pa >= 0; --pa) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa], b[d - pa], acc, 0, 0, 0);
+}
+
+// acc += t one element at a time.  The floatx16 `+=` lowers to v_pk_add_f32,
+// which beside MFMAs costs ~13 cycles more per instruction than the two scalar
+// adds it replaces (MI355X_MICROARCH.md, 'price of one filler beside MFMAs':
+// packed f32 VALU is an anti-lever there); scalar v_add_f32 hide in the MFMA
+// gaps.  Same rounding: one f32 add per element.  The empty asm on each sum
+// keeps the SLP vectorizer from re-packing the adds (it emits no instruction).
+__device__ __forceinline__ void drain(floatx16& acc, const floatx16 t) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float v = acc[r] + t[r];
+        asm("" : "+v"(v));
+        acc[r] = v;
+    }
 }
 
 // the same sum started from zero (one 16-k chunk of the chunked accumulation):
@@ -231,7 +254,7 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_split_kernel(
 #pragma unroll
                         for (int r = 0; r < 16; ++r) tmp[r] = 0.f;
                         mfma_split<NP>(tmp, af[i], bfr[j]);
-                        acc[i][j] += tmp;
+                        drain(acc[i][j], tmp);
                     } else {
                         mfma_split<NP>(acc[i][j], af[i], bfr[j]);
                     }
@@ -525,7 +548,32 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             for (int p = 0; p < NP; ++p)
                 af[i][p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
         }
-        if constexpr (NP == 3 && TN > 2) {
+        if constexpr (NP == 3 && TN > 2 && UBPL_PSA_PP) {
+            // ping-pong chunks: tile q's 6-MFMA chain is issued with tile q-1's
+            // 16 drain adds between its MFMAs (3 VALU slots per MFMA gap), so the
+            // adds hide in the matrix pipe's gaps instead of trailing each chain
+#pragma unroll
+            for (int j = 0; j < TN / 2; ++j) read_b(j);
+            __builtin_amdgcn_sched_barrier(0);
+            floatx16 prev = mfma_split0<NP>(af[0], bfr[0]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = TN / 2; j < TN; ++j) read_b(j);
+#pragma unroll
+            for (int q = 1; q < TM * TN; ++q) {
+                const int j = q / TM, i = q % TM, pj = (q - 1) / TM, pi = (q - 1) % TM;
+                const floatx16 cur = mfma_split0<NP>(af[i], bfr[j]);
+                drain(acc[pi][pj], prev);
+#pragma unroll
+                for (int g = 0; g < 6; ++g) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                prev = cur;
+            }
+            drain(acc[TM - 1][TN - 1], prev);
+        } else if constexpr (NP == 3 && TN > 2) {
             // (no register room for every tile's chunk at once)  The B fragments
             // come in two halves: 18 reads in flight overflow the 4-bit lgkm
             // counter and the compiler then waits for ALL of them before the first
@@ -535,7 +583,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             for (int j = 0; j < TN / 2; ++j) read_b(j);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = 0; i < TM; ++i) acc[i][0] += mfma_split0<NP>(af[i], bfr[0]);
+            for (int i = 0; i < TM; ++i) drain(acc[i][0], mfma_split0<NP>(af[i], bfr[0]));
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = TN / 2; j < TN; ++j) read_b(j);
@@ -544,7 +592,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             for (int j = 1; j < TN; ++j)
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
-                    acc[i][j] += mfma_split0<NP>(af[i], bfr[j]);
+                    drain(acc[i][j], mfma_split0<NP>(af[i], bfr[j]));
                 }
         } else if constexpr (NP == 3) {
 #pragma unroll
@@ -563,7 +611,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] += tmp[i][j];
+                for (int j = 0; j < TN; ++j) drain(acc[i][j], tmp[i][j]);
         } else {
 #pragma unroll
             for (int j = 0; j < TN; ++j) read_b(j);
@@ -634,10 +682,20 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
     constexpr int BH = 8 * BNT * 4 + 128;    // one 8-row half of the B image (+ bank shift)
     constexpr int BB = 2 * BH;
     __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
+    // the prologue's (scale, shift) per input channel (K <= SOL_PRO_K), staged once:
+    // a lane's 8 channels of a K step are 2 ds_read_b128 each, instead of scalar
+    // loads of both 8-channel halves and 16 per-lane selects (48 VALU per K step)
+    __shared__ __attribute__((aligned(16))) float lds_sc[PRO ? SOL_PRO_K : 4], lds_sh[PRO ? SOL_PRO_K : 4];
 
     const int64_t N = (int64_t)B * P;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wn = 64 * wid;
+    if (PRO) {
+        for (int k = tid; k < K; k += NT) {       // visible after the first barrier of the K loop
+            lds_sc[k] = pscale[k];
+            lds_sh[k] = pshift[k];
+        }
+    }
     const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int by = lam % gridDim.y, bx = lam / gridDim.y;
     const int m0 = by * BM;
@@ -701,16 +759,16 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
         if (t + 1 < nkt) stage((t + 1) & 1, (t + 1) * 16);
         const int kt = t * 16;
         const char* base = lds + (t & 1) * (AB + BB);
-        // this lane's k half: 8 (scale, shift) pairs (scalar loads of both halves + selects)
+        // this lane's k half: 8 (scale, shift) pairs
         float sc[8], sh[8];
         if (PRO) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float s0 = pscale[kt + e], s1 = pscale[kt + 8 + e];
-                const float h0 = pshift[kt + e], h1 = pshift[kt + 8 + e];
-                sc[e] = h ? s1 : s0;
-                sh[e] = h ? h1 : h0;
-            }
+            const float4* qs = reinterpret_cast<const float4*>(lds_sc + kt + 8 * h);
+            const float4* qh = reinterpret_cast<const float4*>(lds_sh + kt + 8 * h);
+            const float4 s0 = qs[0], s1 = qs[1], h0 = qh[0], h1 = qh[1];
+            sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+            sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+            sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
+            sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
         }
         const float* bs = reinterpret_cast<const float*>(base + AB + h * BH) + wn + li;
         bf16x8 bfr[TN][NP];
@@ -736,6 +794,35 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
                 bfr[j][p] = __builtin_bit_cast(bf16x8, u);
             }
         }
+#if UBPL_SOL_PP
+        // ping-pong chunks (as conv_psa_kernel): tile (i, j)'s chain is issued
+        // with the previous tile's drain adds between its MFMAs
+        floatx16 prev;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int row = 32 * i + li;
+            bf16x8 af[NP];
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                af[p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const floatx16 cur = mfma_split0<NP>(af, bfr[j]);
+                if (i + j > 0) {
+                    const int q = i * TN + j - 1;
+                    drain(acc[q / TN][q % TN], prev);
+#pragma unroll
+                    for (int g = 0; g < 6; ++g) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                prev = cur;
+            }
+        }
+        drain(acc[TM - 1][TN - 1], prev);
+#else
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int row = 32 * i + li;
@@ -746,11 +833,12 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 // per-chunk accumulation (see conv_fwd_split_kernel)
-                acc[i][j] += mfma_split0<NP>(af, bfr[j]);
+                drain(acc[i][j], mfma_split0<NP>(af, bfr[j]));
             }
             // (register budget: one row block's A fragments live at a time)
             __builtin_amdgcn_sched_barrier(0);
         }
+#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 
@@ -941,7 +1029,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] += tmp[i][j];
+                for (int j = 0; j < TN; ++j) drain(acc[i][j], tmp[i][j]);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -1104,7 +1192,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa64_kernel(const uint16_t* __r
         for (int j = 0; j < TN; ++j) tmp[j] = mfma_split0<NP>(af, bfr[j]);
         __builtin_amdgcn_sched_barrier(0);   // chains first, adds after (see conv_psa_kernel)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[j] += tmp[j];
+        for (int j = 0; j < TN; ++j) drain(acc[j], tmp[j]);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 
@@ -1261,7 +1349,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restri
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] += tmp[i][j];
+            for (int j = 0; j < TN; ++j) drain(acc[i][j], tmp[i][j]);
     }
 
     const int Nt = Cin + 1;
@@ -1712,6 +1800,7 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     if (!sol_supported(B, Cin, Cout, P) || (((uintptr_t)x) & 15) || (((uintptr_t)wsplit) & 15) || (wplane % 8))
         return (int)hipErrorInvalidValue;
     const bool pro = pscale != nullptr;
+    if (pro && Cin > SOL_PRO_K) return (int)hipErrorInvalidValue;
     const int64_t N = (int64_t)B * P;
     const int bm = sol_bm(N, Cout);
     const ubpl::BnBwdEpi bwd{bn_part ? bn_x : nullptr, bn_coef, bn_relu, bn_part};

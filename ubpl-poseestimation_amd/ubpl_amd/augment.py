@@ -125,6 +125,39 @@ def warp_matrix(center, scale, res, angle, W, flip=False):
     return M[:2]
 
 
+def draw_view(kps, W, H, res_in, sf, rf, use_flip=True, use_noise=True):
+    """One view's random draws (python `random`, then torch's CPU
+    generator, in the reference loader's order) and keypoints (numpy [K,3]
+    in, [K,3] out), with the loader's types: keypoints float32 tensors,
+    centre ints, scale and angle float32 0-d tensors.  Host-only (no GPU):
+    -> (2x3 warp matrix flattened, noisy_mean (alpha, beta, on), keypoints)."""
+    kps = torch.tensor(np.asarray(kps, np.float32))
+    center = [int(W / 2), int(H / 2)]                                # utils/process.py:218-221
+    flip = False
+    if use_flip and random.random() <= 0.5:                      # augment.py:218
+        kps[:, 0] = W - kps[:, 0]                                      # process.py:239-242 (float32)
+        center[0] = W - center[0]
+        flip = True
+    noise = (1.0, 0.0, 0.0)
+    if random.random() <= 0.5:                                        # augment.py:262
+        a = random.uniform(0.8, 1.2)
+        b = random.uniform(-0.2, 0.2)
+        noise = (a, b, 1.0 if use_noise else 0.0)
+    scale = torch.tensor(res_in / 200.0)                            # dataset_mds.py:61 (float32)
+    scale = scale * torch.randn(1).mul_(sf).add_(1).clamp(1 - sf, 1 + sf)[0]   # augment.py:19
+    angle = torch.tensor(0.)                                          # dataset_mds.py:60
+    angle = angle + torch.randn(1).mul_(rf).clamp(-rf, rf)[0] \
+        if random.random() <= 1.0 else 0.                              # augment.py:20
+    res = [res_in, res_in]
+    t = get_transform(center, scale, res, rot=angle)
+    out = kps.clone()
+    for k in range(kps.shape[0]):
+        if kps[k, 1] > 0:                                             # augment.py:153
+            out[k, :2] = torch.from_numpy(transform_point(kps[k, :2], t))
+    m = warp_matrix(center, scale, res, angle, W, flip)
+    return m.reshape(-1), noise, out.numpy()
+
+
 class DeviceAugment:
     """imgs: uint8 BGR [N,H,W,3] (numpy or device tensor); means: RGB-ordered
     channel means (MouseData.getSemiData)."""
@@ -139,35 +172,7 @@ class DeviceAugment:
         self.img_mean = Kn.image_mean_u8(self.imgs)
 
     def _draw(self, kps):
-        """One view's random draws and keypoints (numpy [K,3] in, [K,3] out),
-        with the loader's types: keypoints float32 tensors, centre ints,
-        scale and angle float32 0-d tensors."""
-        W, H = self.W, self.H
-        kps = torch.tensor(np.asarray(kps, np.float32))
-        center = [int(W / 2), int(H / 2)]                                # utils/process.py:218-221
-        flip = False
-        if self.use_flip and random.random() <= 0.5:                      # augment.py:218
-            kps[:, 0] = W - kps[:, 0]                                      # process.py:239-242 (float32)
-            center[0] = W - center[0]
-            flip = True
-        noise = (1.0, 0.0, 0.0)
-        if random.random() <= 0.5:                                        # augment.py:262
-            a = random.uniform(0.8, 1.2)
-            b = random.uniform(-0.2, 0.2)
-            noise = (a, b, 1.0 if self.use_noise else 0.0)
-        scale = torch.tensor(self.res / 200.0)                            # dataset_mds.py:61 (float32)
-        scale = scale * torch.randn(1).mul_(self.sf).add_(1).clamp(1 - self.sf, 1 + self.sf)[0]   # augment.py:19
-        angle = torch.tensor(0.)                                          # dataset_mds.py:60
-        angle = angle + torch.randn(1).mul_(self.rf).clamp(-self.rf, self.rf)[0] \
-            if random.random() <= 1.0 else 0.                              # augment.py:20
-        res = [self.res, self.res]
-        t = get_transform(center, scale, res, rot=angle)
-        out = kps.clone()
-        for k in range(kps.shape[0]):
-            if kps[k, 1] > 0:                                             # augment.py:153
-                out[k, :2] = torch.from_numpy(transform_point(kps[k, :2], t))
-        m = warp_matrix(center, scale, res, angle, W, flip)
-        return m.reshape(-1), noise, out.numpy()
+        return draw_view(kps, self.W, self.H, self.res, self.sf, self.rf, self.use_flip, self.use_noise)
 
     def views(self, idx, kps):
         """idx: source image per view [V]; kps: numpy [V,K,3] pixel keypoints.
