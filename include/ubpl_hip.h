@@ -248,14 +248,16 @@ int64_t ubpl_wgrad3_psa_workspace(int B, int Cin, int Cout, int H, int W);
 int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int Cin,
                     int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,
                     void* stream);
-/* 1x1 weight gradient (+ bias gradient, db nullable) on the 6xbf16 path with
+/* 1x1 weight gradient (+ bias gradient, db nullable) on the split path with
  * both f32 operands (dy [B,Cout,P], x [B,Cin,P], prologue relu(x*pscale +
- * pshift) when pscale != nullptr) split while staged.  _workspace: slab floats,
+ * pshift) when pscale != nullptr) split while staged: npieces 3 = 6xbf16,
+ * 1 = bf16 operands with f32 accumulation.  _workspace: slab floats,
  * 0 = shape not supported (needs Cin % 128 == 0, Cout % 128 == 0, P % 16 == 0). */
 int64_t ubpl_wgrad1x1_split_load_workspace(int B, int Cin, int Cout, int P);
 /*@ dy:f32[(int64_t)B*Cout*P] x:f32[(int64_t)B*Cin*P] pscale:f32[Cin] pshift:f32[Cin] slab:f32[ubpl_wgrad1x1_split_load_workspace(B,Cin,Cout,P)] dw:f32[(int64_t)Cout*Cin] db:f32[Cout] */
 int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, int Cin, int Cout, int P, const float* pscale,
-                             const float* pshift, float* slab, float* dw, float* db, int accumulate, void* stream);
+                             const float* pshift, float* slab, float* dw, float* db, int accumulate, int npieces,
+                             void* stream);
 /*@ xs:u16[(npieces-1)*xplane+(int64_t)B*Cin*(H+2*pad)*(W+2*pad)] wsplit:u16[(npieces-1)*wplane+(int64_t)Cout*Cin*KS*KS] bias:f32[Cout] res:f32[(int64_t)B*Cout*H*W] y:f32[(int64_t)B*Cout*H*W] slab:f32[ubpl_conv2d_forward_psa_workspace(B,Cin,Cout,KS,H,W,npieces)] stat_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*H*W)] bn_x:f32[(int64_t)B*Cout*H*W] bn_coef:f32[3*Cout] bn_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*H*W)] */
 int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                             const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
@@ -278,15 +280,16 @@ int ubpl_stem_weight_s2d_split(const float* w, int Cout, int C, int KS, int npie
 /* 1x1 stride-1 conv on the 6xbf16 path with the f32 activations split while
  * they are staged (no pre-split image): y = conv(relu(x*pscale + pshift) or x)
  * + bias (+ res, may alias y); wsplit = 3 planes of [Cout][Cin] from
- * ubpl_conv_weights_split (KS = 1).  Cin % 16 == 0, Cout % 64 == 0, P % 4 == 0.
+ * ubpl_conv_weights_split (KS = 1); npieces 3 = 6xbf16, 1 = bf16 operands (one
+ * plane; no epilogue partials).  Cin % 16 == 0, Cout % 64 == 0, P % 4 == 0.
  * stat_part (nullable): BatchNorm partials of y (ubpl_bn_partials layout).
  * _preferred: 1 when the shape is supported and fills the chip. */
 int ubpl_conv1x1_split_load_preferred(int B, int Cin, int Cout, int P);
-/*@ x:f32[(int64_t)B*Cin*P] wsplit:u16[2*wplane+(int64_t)Cout*Cin] bias:f32[Cout] pscale:f32[Cin] pshift:f32[Cin] res:f32[(int64_t)B*Cout*P] y:f32[(int64_t)B*Cout*P] stat_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*P)] bn_x:f32[(int64_t)B*Cout*P] bn_coef:f32[3*Cout] bn_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*P)] */
+/*@ x:f32[(int64_t)B*Cin*P] wsplit:u16[(npieces-1)*wplane+(int64_t)Cout*Cin] bias:f32[Cout] pscale:f32[Cin] pshift:f32[Cin] res:f32[(int64_t)B*Cout*P] y:f32[(int64_t)B*Cout*P] stat_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*P)] bn_x:f32[(int64_t)B*Cout*P] bn_coef:f32[3*Cout] bn_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*P)] */
 int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int P, const uint16_t* wsplit, int64_t wplane,
                                     const float* bias, int Cout, const float* pscale, const float* pshift,
                                     const float* res, float* y, float* stat_part, const float* bn_x,
-                                    const float* bn_coef, int bn_relu, float* bn_part, void* stream);
+                                    const float* bn_coef, int bn_relu, float* bn_part, int npieces, void* stream);
 
 /* MaxPool2d(2,2) (models/base/layers.py:93), Upsample(x2, nearest) + add
  * (layers.py:110-111), AvgPool2d(2,2) projection (models/pose/hourglass.py:226). */

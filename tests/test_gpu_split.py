@@ -207,6 +207,68 @@ def test_bf16_wgrad3_psa_vs_rounded_f64(case):
     assert _rel(db, dbref) <= 1e-5
 
 
+@pytest.mark.parametrize("case", [(2, 256, 64, 128, True, True), (2, 128, 32, 256, True, False),
+                                  (3, 64, 16, 64, False, True)])
+def test_bf16_conv1x1_split_load_vs_rounded_f64(case):
+    """conv1x1_sol_kernel with NP = 1 (the "bf16" precision's 1x1 convs where the
+    plane fills the chip: no pre-split pass): forward with prologue / residual
+    and the data gradient equal float64 on the bf16-rounded (RNE) operands to
+    f32 summation error, like the PSA kernels with NP = 1."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, H, Cout, pro, resid = case
+    gen = torch.Generator().manual_seed(61 + hash(case) % 1000)
+    x32 = torch.randn(B, Cin, H, H, generator=gen)
+    w32 = torch.randn(Cout, Cin, 1, 1, generator=gen) / np.sqrt(Cin)
+    b32 = torch.randn(Cout, generator=gen)
+    sc32 = torch.rand(Cin, generator=gen) + 0.5
+    sh32 = torch.randn(Cin, generator=gen) * 0.5
+    res32 = torch.randn(B, Cout, H, H, generator=gen) if resid else None
+    bf = lambda t: t.to(torch.bfloat16).double()
+    inp = F.relu((x32.double() * sc32.double()[None, :, None, None] + sh32.double()[None, :, None, None]).float()) \
+        if pro else x32
+    yref = F.conv2d(bf(inp), bf(w32), b32.double())
+    if resid:
+        yref = yref + res32.double()
+    d = lambda t: None if t is None else t.to(DEV)
+    ps, ph = (d(sc32), d(sh32)) if pro else (None, None)
+    y = Kn.conv1x1_forward_split_load(d(x32), Kn.conv_weight_split(d(w32), 0, 1), d(b32), ps, ph, res=d(res32))
+    e = _rel(y, yref)
+    print("bf16 sol fwd %s: %.2e" % (case, e))
+    assert e <= 2e-6, e
+    if Cin % 64 == 0:
+        dy = torch.randn(B, Cout, H, H, generator=gen)
+        dxref = torch.nn.grad.conv2d_input((B, Cin, H, H), bf(w32), bf(dy))
+        dx = Kn.conv1x1_forward_split_load(d(dy), Kn.conv_weight_split(d(w32), 1, 1), None)
+        e = _rel(dx, dxref)
+        print("bf16 sol dgrad %s: %.2e" % (case, e))
+        assert e <= 2e-6, e
+
+
+@pytest.mark.parametrize("case", [(2, 256, 128, 64, True), (3, 128, 256, 16, False)])
+def test_bf16_wgrad1x1_split_load_vs_rounded_f64(case):
+    """1x1 weight gradient with NP = 1 (bf16 operands, f32 accumulation) vs
+    float64 of the bf16-rounded operands; the bias gradient sums the f32 dy."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, Cout, H, pro = case
+    gen = torch.Generator().manual_seed(67 + hash(case) % 1000)
+    x = torch.randn(B, Cin, H, H, generator=gen)
+    dy = torch.randn(B, Cout, H, H, generator=gen)
+    sc, sh = torch.rand(Cin, generator=gen) + 0.5, torch.randn(Cin, generator=gen) * 0.5
+    bf = lambda t: t.to(torch.bfloat16).double()
+    inp = F.relu((x.double() * sc.double()[None, :, None, None] + sh.double()[None, :, None, None]).float()) \
+        if pro else x
+    dwref = torch.nn.grad.conv2d_weight(bf(inp), (Cout, Cin, 1, 1), bf(dy))
+    dbref = dy.double().sum((0, 2, 3))
+    d = lambda t: t.to(DEV)
+    ps, ph = (d(sc), d(sh)) if pro else (None, None)
+    dw, db = torch.zeros(Cout, Cin, 1, 1, device=DEV), torch.zeros(Cout, device=DEV)
+    Kn.conv2d_wgrad1x1_split_load(d(dy), d(x), dw, db, ps, ph, accumulate=False, npieces=1)
+    e = _rel(dw, dwref)
+    print("bf16 wgrad1 %s: %.2e" % (case, e))
+    assert e <= 2e-6, e
+    assert _rel(db, dbref) <= 1e-5
+
+
 def test_split_activation_layout():
     """PSA image: pieces sum back to relu(x*s+h) exactly, border zero, [B][C/16][Hp][Wp][16]."""
     from ubpl_amd import kernels as Kn

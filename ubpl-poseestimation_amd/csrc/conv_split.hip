@@ -668,7 +668,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 // planes of [M][K] (ubpl_conv_weights_split with KS = 1), staged as in
 // conv_psa_kernel.  2-stage ring, 2 workgroups per CU.  The activation read is
 // the f32 tensor itself: no split pass, no 6-byte/element PSA image.
-template <int BM, bool PRO, bool EPI = false>
+template <int BM, bool PRO, bool EPI = false, int NP = 3>
 __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restrict__ x,
                                                            const uint16_t* __restrict__ wp, int64_t wplane,
                                                            const float* __restrict__ bias,
@@ -676,7 +676,9 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
                                                            const float* __restrict__ pshift, const float* res,
                                                            float* y, int B, int K, int P, int M,
                                                            float* __restrict__ stat_part, ubpl::BnBwdEpi bwd) {
-    constexpr int NP = 3, BNT = 256, NS = 2;
+    // NP = 3: 6xbf16 (f32-equivalent); NP = 1: the "bf16" precision (operands
+    // rounded to bf16, one MFMA per product, accumulated in f32 directly)
+    constexpr int BNT = 256, NS = 2;
     constexpr int TM = BM / 32, TN = 2;
     constexpr int AB = NP * BM * 32;         // A stage bytes: [piece][BM rows][32 B]
     constexpr int BH = 8 * BNT * 4 + 128;    // one 8-row half of the B image (+ bank shift)
@@ -794,6 +796,16 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
                 bfr[j][p] = __builtin_bit_cast(bf16x8, u);
             }
         }
+        if constexpr (NP == 1) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int row = 32 * i + li;
+                bf16x8 af[NP];
+                af[0] = *reinterpret_cast<const bf16x8*>(base + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+#pragma unroll
+                for (int j = 0; j < TN; ++j) mfma_split<NP>(acc[i][j], af, bfr[j]);
+            }
+        } else {
 #if UBPL_SOL_PP
         // ping-pong chunks (as conv_psa_kernel): tile (i, j)'s chain is issued
         // with the previous tile's drain adds between its MFMAs
@@ -839,6 +851,7 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
             __builtin_amdgcn_sched_barrier(0);
         }
 #endif
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 
@@ -1226,12 +1239,13 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa64_kernel(const uint16_t* __r
 // the pieces go to a double-buffered LDS image [operand][piece][128 rows][32 B]
 // (chunk swizzle c ^ ((row >> 3) & 1), conflict-free ds_read_b128 fragments,
 // conv_psa_kernel's layout).  Tile 128 x 128, wave tile 64 x 64.
-template <bool PRO>
+template <bool PRO, int NP = 3>
 __global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                           const float* __restrict__ pscale,
                                                           const float* __restrict__ pshift, int B, int Cin, int Cout,
                                                           int P, int steps_per_split, float* __restrict__ slab) {
-    constexpr int NP = 3, BM = 128, TM = 2, TN = 2;
+    // NP = 3: 6xbf16; NP = 1: bf16 operands, f32 accumulation (the "bf16" precision)
+    constexpr int BM = 128, TM = 2, TN = 2;
     constexpr int PI = BM * 32;   // one piece image: 128 rows x 16 pixels x 2 B
     constexpr int OB = NP * PI;   // one operand
     constexpr int SB = 2 * OB;    // one stage: dy pieces, then x pieces
@@ -1338,18 +1352,25 @@ __global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restri
                 bfr[j][p] =
                     *reinterpret_cast<const bf16x8*>(base + OB + p * PI + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
         }
-        floatx16 tmp[TM][TN];
+        if constexpr (NP == 1) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                tmp[i][j] = mfma_split0<NP>(af[i], bfr[j]);
-            }
-        __builtin_amdgcn_sched_barrier(0);   // chains first, adds after (see conv_psa_kernel)
+                for (int j = 0; j < TN; ++j) mfma_split<NP>(acc[i][j], af[i], bfr[j]);
+        } else {
+            floatx16 tmp[TM][TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) drain(acc[i][j], tmp[i][j]);
+                for (int j = 0; j < TN; ++j) {
+                    tmp[i][j] = mfma_split0<NP>(af[i], bfr[j]);
+                }
+            __builtin_amdgcn_sched_barrier(0);   // chains first, adds after (see conv_psa_kernel)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) drain(acc[i][j], tmp[i][j]);
+        }
     }
 
     const int Nt = Cin + 1;
@@ -1795,9 +1816,10 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
                                              int64_t wplane, const float* bias, int Cout, const float* pscale,
                                              const float* pshift, const float* res, float* y, float* stat_part,
                                              const float* bn_x, const float* bn_coef, int bn_relu, float* bn_part,
-                                             void* stream) {
+                                             int npieces, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    if (!sol_supported(B, Cin, Cout, P) || (((uintptr_t)x) & 15) || (((uintptr_t)wsplit) & 15) || (wplane % 8))
+    if (!sol_supported(B, Cin, Cout, P) || (((uintptr_t)x) & 15) || (((uintptr_t)wsplit) & 15) || (wplane % 8) ||
+        (npieces != 1 && npieces != 3))
         return (int)hipErrorInvalidValue;
     const bool pro = pscale != nullptr;
     if (pro && Cin > SOL_PRO_K) return (int)hipErrorInvalidValue;
@@ -1806,9 +1828,13 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     const ubpl::BnBwdEpi bwd{bn_part ? bn_x : nullptr, bn_coef, bn_relu, bn_part};
     dim3 grid((unsigned)((N + 255) / 256), (unsigned)(Cout / bm));
     const bool epi = stat_part != nullptr || bn_part != nullptr;
+    if (epi && npieces == 1) return (int)hipErrorInvalidValue;   // (epilogue partials: 6xbf16 only)
 #define UBPL_SOL(BM_, PRO_)                                                                                       \
     do {                                                                                                          \
-        if (epi)                                                                                                  \
+        if (npieces == 1)                                                                                         \
+            hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 1>), grid, dim3(NT), 0, st, x, wsplit,       \
+                               wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);              \
+        else if (epi)                                                                                             \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, true>), grid, dim3(NT), 0, st, x, wsplit, wplane,   \
                                bias, pscale, pshift, res, y, B, Cin, P, Cout, stat_part, bwd);                    \
         else                                                                                                      \
@@ -1917,21 +1943,27 @@ UBPL_API int64_t ubpl_wgrad1x1_split_load_workspace(int B, int Cin, int Cout, in
 // when pscale != nullptr.  16-B aligned dy / x.
 UBPL_API int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, int Cin, int Cout, int P,
                                       const float* pscale, const float* pshift, float* slab, float* dw, float* db,
-                                      int accumulate, void* stream) {
+                                      int accumulate, int npieces, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (!wgrad1_sol_supported(B, Cin, Cout, P) || slab == nullptr || (((uintptr_t)dy) & 15) ||
-        (((uintptr_t)x) & 15))
+        (((uintptr_t)x) & 15) || (npieces != 1 && npieces != 3))
         return (int)hipErrorInvalidValue;
     const int splits = wgrad1_sol_splits(B, Cin, Cout, P);
     const int steps = B * (P / 16);
     const int per = (steps + splits - 1) / splits;
     dim3 grid((unsigned)(Cin / 128), (unsigned)(Cout / 128), (unsigned)splits);
-    if (pscale != nullptr)
+    if (pscale != nullptr && npieces == 3)
         hipLaunchKernelGGL((wgrad1_sol_kernel<true>), grid, dim3(NT), 0, st, dy, x, pscale, pshift, B, Cin, Cout, P,
                            per, slab);
-    else
+    else if (npieces == 3)
         hipLaunchKernelGGL((wgrad1_sol_kernel<false>), grid, dim3(NT), 0, st, dy, x, pscale, pshift, B, Cin, Cout, P,
                            per, slab);
+    else if (pscale != nullptr)
+        hipLaunchKernelGGL((wgrad1_sol_kernel<true, 1>), grid, dim3(NT), 0, st, dy, x, pscale, pshift, B, Cin, Cout,
+                           P, per, slab);
+    else
+        hipLaunchKernelGGL((wgrad1_sol_kernel<false, 1>), grid, dim3(NT), 0, st, dy, x, pscale, pshift, B, Cin, Cout,
+                           P, per, slab);
     UBPL_LAUNCH_CHECK();
     return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 1, db != nullptr, dw, db, accumulate, stream);
 }

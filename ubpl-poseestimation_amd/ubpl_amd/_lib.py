@@ -62,7 +62,7 @@ SIGNATURES = {
     "ubpl_wgrad3_psa_workspace": (L, [I, I, I, I, I]),
     "ubpl_wgrad3_psa": (I, [P, L, P, L, I, I, I, I, I, P, P, P, I, I, P]),
     "ubpl_wgrad1x1_split_load_workspace": (L, [I, I, I, I]),
-    "ubpl_wgrad1x1_split_load": (I, [P, P, I, I, I, I, P, P, P, P, P, I, P]),
+    "ubpl_wgrad1x1_split_load": (I, [P, P, I, I, I, I, P, P, P, P, P, I, I, P]),
     "ubpl_conv2d_forward_split_workspace": (L, [I, I, I, I, I, I, I]),
     "ubpl_conv2d_forward_split": (I, [P, I, I, I, I, P, L, P, I, I, I, P, P, P, P, I, I, P, I, P]),
     "ubpl_conv_weights_split": (I, [P, P, L, P, I, I, I, P]),
@@ -72,7 +72,7 @@ SIGNATURES = {
     "ubpl_stem_s2d_split": (I, [P, I, I, I, I, I, I, P, L, P]),
     "ubpl_stem_weight_s2d_split": (I, [P, I, I, I, I, P, L, P]),
     "ubpl_conv1x1_split_load_preferred": (I, [I, I, I, I]),
-    "ubpl_conv1x1_forward_split_load": (I, [P, I, I, I, P, L, P, I, P, P, P, P, P, P, P, I, P, P]),
+    "ubpl_conv1x1_forward_split_load": (I, [P, I, I, I, P, L, P, I, P, P, P, P, P, P, P, I, P, I, P]),
     "ubpl_maxpool2x2_forward": (I, [P, L, I, I, P, P]),
     "ubpl_maxpool2x2_backward": (I, [P, P, L, I, I, P, I, P]),
     "ubpl_avgpool2x2_forward": (I, [P, L, I, I, P, P]),

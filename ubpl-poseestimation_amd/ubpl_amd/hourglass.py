@@ -47,6 +47,9 @@ _STEM_S2D = os.environ.get("UBPL_STEM_S2D", "1") != "0"
 # epilogue partials + a finalize launch measured 1.3 % slower than the one-launch
 # statistics pass (stats_kernel) on the training step.
 _FWD_EPI = os.environ.get("UBPL_FWD_EPI", "0") == "1"
+# diagnostic (tools/graph_fwd_probe.py locate): the hourglass upsample-add out of place, its
+# up1 input saved, so a graph replay's first wrong activation can name up1 or the add
+_UPADD_OOP = os.environ.get("UBPL_UPADD_OOP", "0") == "1"
 
 
 # ---------------------------------------------------------------------------
@@ -245,9 +248,13 @@ class StackedHourglass(nn.Module):
                  split while they are staged, the rest f32;
         '3xbf16' every conv with 16-channel contraction groups on the 2-piece
                  register-staged split kernel (faster, ~2^-16 operands: not parity-grade);
-        'bf16'   every conv with 16-channel contraction groups (3x3 and 1x1, all three
-                 directions) on the PSA kernels with ONE piece per operand = bf16
-                 operands, f32 accumulation (BASELINE config 5's throughput path).
+        'bf16'   every conv with 16-channel contraction groups (3x3 and 1x1, forward
+                 and data gradient) with ONE piece per operand = bf16 operands, f32
+                 accumulation (BASELINE config 5's throughput path): 1x1 convs whose
+                 plane fills the chip on the split-on-load kernel (no pre-split pass),
+                 the rest on the PSA kernels; weight gradients on the PSA (3x3) and
+                 split-on-load (1x1, 128-multiple channels) kernels, the other 1x1
+                 weight gradients exact f32.
         The stem (7x7, stride 2, 3 input channels) runs in f32 except on the
         6xbf16 space-to-depth path."""
         self.conv_pieces = Kn.conv_precision_pieces(name)
@@ -573,11 +580,12 @@ class _Exec:
         mkpart = lambda: (Kn.bn_partial_buffer(Cout, B * x.shape[2] * x.shape[3], x.device)
                           if stats and _FWD_EPI else None)
         ws = self.m.SW(0, name + ".weight") if stride == 1 else None
-        if ws is not None and ws.npieces == 3 and ws.shape[1] == 1:
+        if ws is not None and ws.npieces in (1, 3) and ws.shape[1] == 1:
             if Kn.conv1x1_split_load_ok(x, ws):
-                part = mkpart()
+                part = mkpart() if ws.npieces == 3 else None
                 return Kn.conv1x1_forward_split_load(x, ws, b, ps, ph, res=res, out=out, stat_part=part), part
-            ws = None                                    # small plane: the f32 1x1 kernel
+            if ws.npieces == 3:
+                ws = None                                # small plane: the f32 1x1 kernel (bf16: the PSA kernel)
         if ws is not None:
             if ws.npieces in (1, 3):
                 part = mkpart()
@@ -642,6 +650,11 @@ class _Exec:
         low3 = self.residual(p + ".low3", low2)
         self.save(p, x)
         part = self.stat_buffer(up1.shape)
+        if _UPADD_OOP:                                   # diagnostic: up1 kept, the sum in a new tensor
+            self.save(p + ".up1_out", up1)
+            out = Kn.upsample2x_add(up1, low3, stat_part=part)
+            self.give_part(out, part)
+            return out
         out = Kn.upsample2x_add(up1, low3, out=up1, stat_part=part)
         self.give_part(out, part)
         return out
@@ -669,9 +682,9 @@ class _Exec:
 
     def wgrad(self, name, dy, x, KS, stride=1, pro=None):
         ps, ph = (None, None) if pro is None else pro
-        if KS == 1 and self.m.conv_pieces == 3 and _WGRAD1_SPLIT and Kn.wgrad1x1_split_load_ok(dy, x):
+        if KS == 1 and self.m.conv_pieces in (1, 3) and _WGRAD1_SPLIT and Kn.wgrad1x1_split_load_ok(dy, x):
             Kn.conv2d_wgrad1x1_split_load(dy, x, self.G(name + ".weight"), self.G(name + ".bias"), ps, ph,
-                                          accumulate=True)
+                                          accumulate=True, npieces=self.m.conv_pieces)
             return
         Kn.conv2d_wgrad(dy, x, KS, stride, self.G(name + ".weight"), self.G(name + ".bias"), ps, ph,
                         accumulate=True)
@@ -688,12 +701,13 @@ class _Exec:
         """bnb = (bn, x): the result is dz of BN bn (input x) — returns (dx, its
         backward partials or None); else dx."""
         ws = self.m.SW(1, name + ".weight")
-        if ws is not None and ws.npieces == 3 and ws.shape[1] == 1:
+        if ws is not None and ws.npieces in (1, 3) and ws.shape[1] == 1:
             if Kn.conv1x1_split_load_ok(dy, ws):
-                bwd, part = self.bwd_epi(*(bnb or (None, None)))
+                bwd, part = self.bwd_epi(*(bnb or (None, None))) if ws.npieces == 3 else (None, None)
                 y = Kn.conv1x1_forward_split_load(dy, ws, None, res=res, out=out, bwd=bwd)
                 return (y, part) if bnb is not None else y
-            ws = None
+            if ws.npieces == 3:
+                ws = None
         if bnb is not None:
             return self.dgrad(name, dy, res=res, out=out), None
         if ws is not None:

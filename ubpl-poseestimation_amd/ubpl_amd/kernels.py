@@ -359,15 +359,16 @@ def wgrad1x1_split_load_ok(dy, x):
             and _lib.lib().ubpl_wgrad1x1_split_load_workspace(B, Cin, dy.shape[1], H * W) > 0)
 
 
-def conv2d_wgrad1x1_split_load(dy, x, dw, db, pscale=None, pshift=None, accumulate=True):
-    """1x1 weight (+ bias) gradient on the 6xbf16 path, f32 operands split on load
-    (v = relu(x*pscale + pshift) when pscale is given)."""
+def conv2d_wgrad1x1_split_load(dy, x, dw, db, pscale=None, pshift=None, accumulate=True, npieces=3):
+    """1x1 weight (+ bias) gradient on the split path (npieces 3: 6xbf16; 1: bf16
+    operands, f32 accumulation), f32 operands split on load (v = relu(x*pscale +
+    pshift) when pscale is given)."""
     B, Cin, H, W = x.shape
     Cout = dy.shape[1]
     n = _lib.lib().ubpl_wgrad1x1_split_load_workspace(B, Cin, Cout, H * W)
     slab = torch.empty(int(n), device=x.device, dtype=F32)
     call("ubpl_wgrad1x1_split_load", _p(dy), _p(x), B, Cin, Cout, H * W, _p(pscale), _p(pshift), _p(slab), _p(dw),
-         _p(db), int(accumulate))
+         _p(db), int(accumulate), int(npieces))
 
 
 def conv_weight_flip(w):
@@ -524,9 +525,9 @@ _NO_SOL = os.environ.get("UBPL_NO_SOL") == "1"      # diagnostic: every 1x1 on t
 
 
 def conv1x1_split_load_ok(x, ws):
-    """The 6xbf16 split-on-load 1x1 kernel takes this shape and fills the chip."""
+    """The split-on-load 1x1 kernel (6xbf16 or bf16) takes this shape and fills the chip."""
     B, Cin, H, W = x.shape
-    return (not _NO_SOL and ws is not None and ws.npieces == 3 and ws.shape[1] == 1 and ws.shape[2] == Cin
+    return (not _NO_SOL and ws is not None and ws.npieces in (1, 3) and ws.shape[1] == 1 and ws.shape[2] == Cin
             and x.data_ptr() % 16 == 0
             and bool(_lib.lib().ubpl_conv1x1_split_load_preferred(B, Cin, ws.shape[0], H * W)))
 
@@ -542,18 +543,19 @@ def _bnb(bwd):
 
 def conv1x1_forward_split_load(x, ws, bias, pscale=None, pshift=None, res=None, out=None, stat_part=None,
                                bwd=None):
-    """1x1 stride-1 conv on the 6xbf16 path with x (NCHW f32) split while it is
-    staged: y = conv(relu(x*pscale + pshift) or x, ws) + bias (+ res; res may
+    """1x1 stride-1 conv on the split path (ws.npieces 3: 6xbf16; 1: bf16 operands)
+    with x (NCHW f32) split while it is staged: y = conv(relu(x*pscale + pshift) or x, ws) + bias (+ res; res may
     alias out); ws = SplitWeights (rows, 1, Cin) — a forward (mode 0) or a data
     gradient (mode 1, x = dy) table; stat_part: BatchNorm partials of y."""
     B, Cin, H, W = x.shape
     Cout, T, wc = ws.shape
-    if T != 1 or wc != Cin or ws.npieces != 3:
+    if T != 1 or wc != Cin or ws.npieces not in (1, 3) or (ws.npieces == 1 and (stat_part is not None or
+                                                                            bwd is not None)):
         raise AssertionError("split-load 1x1: weights {} / pieces {} for {} input channels".format(
             ws.shape, ws.npieces, Cin))
     y = torch.empty((B, Cout, H, W), device=x.device, dtype=F32) if out is None else out
     call("ubpl_conv1x1_forward_split_load", _p(x), B, Cin, H * W, ws.ptr(), int(ws.plane), _p(bias), Cout,
-         _p(pscale), _p(pshift), _p(res), _p(y), _p(stat_part), *_bnb(bwd))
+         _p(pscale), _p(pshift), _p(res), _p(y), _p(stat_part), *_bnb(bwd), int(ws.npieces))
     return y
 
 
