@@ -334,6 +334,18 @@ int ubpl_image_mean_u8(const uint8_t* imgs, int N, int64_t n_per_image, float* o
 int ubpl_augment_warp(const uint8_t* imgs, int H, int W, const int* src_idx, const float* mat, const float* noise,
                       const float* img_mean, const float* chan_mean, int V, int Ho, int Wo, float* out, void* stream);
 
+/* Random occlusion of augmented views (utils/udaap/utils_augment.py:21-25,116-163:
+ * augment_occlu / occlude_with_objects / resize_by_factor / paste_over), after
+ * ubpl_augment_warp: out [V][3][H][W] (colorNorm'ed) gets, in draw order, each
+ * paste alpha * (color - chan_mean) + (1 - alpha) * out.  bank: RGBA float
+ * occluders (16-B aligned, [h][w][4] each at bank + off[o], hw[2o..2o+1] = h, w);
+ * pastes int [P][9] = (view, occluder, w1, h1, x0, y0, x1, y1, sx0 | sy0 << 16)
+ * sorted by view, view_first [V+1] the first paste of each view; the occluder is
+ * resized to w1 x h1 by pixel-area averaging (cv2.INTER_AREA). */
+/*@ out:f32[(int64_t)V*3*H*W] bank:f32[?] off:i64[?] hw:i32[?] pastes:i32[?] view_first:i32[V+1] chan_mean:f32[3] */
+int ubpl_occlude(float* out, int V, int H, int W, const float* bank, const int64_t* off, const int* hw,
+                 const int* pastes, const int* view_first, const float* chan_mean, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

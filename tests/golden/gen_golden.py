@@ -230,6 +230,21 @@ def gen_augment(R):
     np.savez_compressed(os.path.join(HERE, "augment.npz"), **out)
 
 
+def gen_occlusion(R):
+    """f1 occlusion: the reference's own paste_over (utils/udaap/utils_augment.py:
+    131-163) on synthetic occluders and images (Augment.__init__ needs Pascal VOC
+    and resize_by_factor needs cv2 — both absent — so the pastes are made with
+    already-sized occluders): pins the clipping geometry and the blend."""
+    import utils.udaap.utils_augment as UA
+    aug = object.__new__(UA.Augment)
+    out = {}
+    for cname, (dst, occ, center) in seeds.occlusion_cases().items():
+        d = dst.copy()
+        aug.paste_over(im_src=occ, im_dst=d, center=np.asarray(center, np.float64))
+        out[cname + "/out"] = d
+    np.savez_compressed(os.path.join(HERE, "occlusion.npz"), **out)
+
+
 # --------------------------------------------------------------------------
 # H1-H6 hourglass forward/backward
 # --------------------------------------------------------------------------
@@ -366,7 +381,7 @@ def _flatten(x):
 if __name__ == "__main__":
     torch.set_num_threads(8)
     R = import_reference()
-    which = sys.argv[1:] or ["render", "losses", "decode", "misc", "augment", "hourglass", "steps"]
+    which = sys.argv[1:] or ["render", "losses", "decode", "misc", "augment", "occlusion", "hourglass", "steps"]
     for w in which:
         print("generating", w, flush=True)
         globals()["gen_" + w](R)

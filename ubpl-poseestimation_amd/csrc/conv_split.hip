@@ -668,7 +668,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 // planes of [M][K] (ubpl_conv_weights_split with KS = 1), staged as in
 // conv_psa_kernel.  2-stage ring, 2 workgroups per CU.  The activation read is
 // the f32 tensor itself: no split pass, no 6-byte/element PSA image.
-template <int BM, bool PRO, bool EPI = false, int NP = 3>
+template <int BM, bool PRO, bool EPI = false, int NP = 3, int NS = 2>
 __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restrict__ x,
                                                            const uint16_t* __restrict__ wp, int64_t wplane,
                                                            const float* __restrict__ bias,
@@ -678,7 +678,8 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
                                                            float* __restrict__ stat_part, ubpl::BnBwdEpi bwd) {
     // NP = 3: 6xbf16 (f32-equivalent); NP = 1: the "bf16" precision (operands
     // rounded to bf16, one MFMA per product, accumulated in f32 directly)
-    constexpr int BNT = 256, NS = 2;
+    // NS: stages in the LDS ring (2, or 3 with 64-row tiles: two K steps' DMA in flight)
+    constexpr int BNT = 256;
     constexpr int TM = BM / 32, TN = 2;
     constexpr int AB = NP * BM * 32;         // A stage bytes: [piece][BM rows][32 B]
     constexpr int BH = 8 * BNT * 4 + 128;    // one 8-row half of the B image (+ bank shift)
@@ -753,14 +754,21 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
 
     const int nkt = K >> 4;
     stage(0, 0);
+    if (NS == 3 && nkt > 1) stage(1, 16);
     for (int t = 0; t < nkt; ++t) {
-        // stage t landed for every wave, every wave done with stage t-1
-        vm_wait<0>();
+        // stage t landed for every wave (NS = 3: this wave's stage t+1 DMA may stay in
+        // flight), every wave done with stage t-1
+        if (NS == 3 && t + 1 < nkt) {
+            if (a_issue) vm_wait<NP + 4>();
+            else vm_wait<4>();
+        } else {
+            vm_wait<0>();
+        }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (t + 1 < nkt) stage((t + 1) & 1, (t + 1) * 16);
+        if (t + NS - 1 < nkt) stage((t + NS - 1) % NS, (t + NS - 1) * 16);
         const int kt = t * 16;
-        const char* base = lds + (t & 1) * (AB + BB);
+        const char* base = lds + (t % NS) * (AB + BB);
         // this lane's k half: 8 (scale, shift) pairs
         float sc[8], sh[8];
         if (PRO) {
@@ -1794,8 +1802,14 @@ bool sol_supported(int B, int Cin, int Cout, int P) {
 // Output-channel block: 128 rows (each pixel tile split once per 128 channels)
 // unless that leaves CUs idle; then 64 (the 32x32-plane 256->128 convs at B=32:
 // 128 -> 256 workgroups).
+// UBPL_SOL_BM=64: 64-row tiles everywhere (A/B knob); UBPL_SOL_NS=3: 3-stage ring on 64-row tiles
+static int sol_env(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
 static int sol_bm(int64_t N, int Cout) {
-    if (Cout % 128 != 0) return 64;
+    static const int force = sol_env("UBPL_SOL_BM", 0);
+    if (Cout % 128 != 0 || force == 64) return 64;
     return ((N + 255) / 256) * (Cout / 128) >= occ_info().ncu ? 128 : 64;
 }
 
@@ -1829,10 +1843,14 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     dim3 grid((unsigned)((N + 255) / 256), (unsigned)(Cout / bm));
     const bool epi = stat_part != nullptr || bn_part != nullptr;
     if (epi && npieces == 1) return (int)hipErrorInvalidValue;   // (epilogue partials: 6xbf16 only)
+    static const bool ns3 = sol_env("UBPL_SOL_NS", 2) == 3;
 #define UBPL_SOL(BM_, PRO_)                                                                                       \
     do {                                                                                                          \
         if (npieces == 1)                                                                                         \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 1>), grid, dim3(NT), 0, st, x, wsplit,       \
+                               wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);              \
+        else if (BM_ == 64 && ns3 && !epi)                                                                        \
+            hipLaunchKernelGGL((conv1x1_sol_kernel<64, PRO_, false, 3, 3>), grid, dim3(NT), 0, st, x, wsplit,     \
                                wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);              \
         else if (epi)                                                                                             \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, true>), grid, dim3(NT), 0, st, x, wsplit, wplane,   \

@@ -158,6 +158,128 @@ def draw_view(kps, W, H, res_in, sf, rf, use_flip=True, use_noise=True):
     return m.reshape(-1), noise, out.numpy()
 
 
+# ---------------------------------------------------------------------------
+# random occlusion (utils/udaap/utils_augment.py) — off by default in the
+# reference (useOcclusion False, projects/MT_UBPL.py:473)
+# ---------------------------------------------------------------------------
+def _ellipse_8x8():
+    """cv2.getStructuringElement(cv2.MORPH_ELLIPSE, (8, 8)) (OpenCV's row-span rule:
+    r = c = 4, row i spans c -+ round(sqrt(r^2 - (i - r)^2)))."""
+    k = np.zeros((8, 8), bool)
+    for i in range(8):
+        dy = i - 4
+        dx = int(round(4 * np.sqrt((16 - dy * dy) / 16.0)))
+        k[i, max(4 - dx, 0):min(4 + dx + 1, 8)] = True
+    return k
+
+
+def _erode(mask, k):
+    """cv2.erode with kernel k, anchor at its centre, constant border = +inf."""
+    from scipy.ndimage import grey_erosion
+    return grey_erosion(mask, footprint=k, mode="constant", cval=255, origin=(-0, -0))
+
+
+def _area_half(img):
+    """cv2.resize(..., fx=fy=0.5, INTER_AREA) of a uint8 image: 2x2 means, (s + 2) >> 2."""
+    h, w = img.shape[0] // 2, img.shape[1] // 2
+    s = (img[0:2 * h:2, 0:2 * w:2].astype(np.int32) + img[1:2 * h:2, 0:2 * w:2] + img[0:2 * h:2, 1:2 * w:2] +
+         img[1:2 * h:2, 1:2 * w:2])
+    return ((s + 2) >> 2).astype(np.uint8)
+
+
+class OcclusionBank:
+    """The occluders of Augment (utils/udaap/utils_augment.py:13-88), resident on
+    the device: RGBA float images in [0,1] (the object's pixels + a mask whose
+    border ring is 192, downscaled by 0.5).  `from_voc` restates load_occluders
+    on a Pascal VOC 2012 tree (segmented objects that are not cat / dog / cow /
+    horse / sheep / person, >= 500 mask pixels); cv2 is not in this image, so
+    the 8x8 elliptic erosion and the INTER_AREA halving are restated (parity
+    unpinned).  Any list of RGBA float arrays works as a bank."""
+
+    def __init__(self, occluders, device="cuda"):
+        if not occluders:
+            raise ValueError("OcclusionBank: no occluders")
+        offs, flat, o = [], [], 0
+        for a in occluders:
+            a = np.ascontiguousarray(a, np.float32)
+            if a.ndim != 3 or a.shape[2] != 4:
+                raise ValueError("OcclusionBank: occluders are [h, w, 4] RGBA")
+            offs.append(o)
+            flat.append(a.reshape(-1))
+            o += a.size
+        self.sizes = [tuple(a.shape[:2]) for a in occluders]
+        self.dev = torch.device(device)
+        self.bank = torch.from_numpy(np.concatenate(flat)).to(self.dev)
+        self.off = torch.tensor(offs, dtype=torch.int64, device=self.dev)
+        self.hw = torch.tensor([v for hw in self.sizes for v in hw], dtype=torch.int32, device=self.dev)
+
+    @classmethod
+    def from_voc(cls, voc_root, device="cuda"):
+        import os
+        import xml.etree.ElementTree as ET
+        from PIL import Image
+        k = _ellipse_8x8()
+        skip = {"cat", "dog", "cow", "horse", "sheep", "person"}
+        occ = []
+        ann = os.path.join(voc_root, "Annotations")
+        for name in sorted(os.listdir(ann)):
+            root = ET.parse(os.path.join(ann, name)).getroot()
+            if root.find("segmented").text == "0":
+                continue
+            boxes = [(i, [int(o.find("bndbox").find(t).text) for t in ("xmin", "ymin", "xmax", "ymax")])
+                     for i, o in enumerate(root.findall("object")) if o.find("name").text not in skip]
+            if not boxes:
+                continue
+            fn = root.find("filename").text
+            im = np.asarray(Image.open(os.path.join(voc_root, "JPEGImages", fn)))
+            labels = np.asarray(Image.open(os.path.join(voc_root, "SegmentationObject", fn.replace("jpg", "png"))))
+            for i, (x0, y0, x1, y1) in boxes:
+                mask = (labels[y0:y1, x0:x1] == i + 1).astype(np.uint8) * 255
+                if int((mask > 0).sum()) < 500:
+                    continue
+                mask[_erode(mask, k) < mask] = 192
+                rgba = np.concatenate([im[y0:y1, x0:x1], mask[..., None]], axis=-1)
+                occ.append(_area_half(rgba).astype(np.float32) / 255.0)
+        return cls(occ, device)
+
+
+def draw_occlusion(W, H, sizes, aug_rate=0.5, num_occluder=8):
+    """One view's occlusion draws with the reference's RNG calls, in its order
+    (augment_occlu :21-25, occlude_with_objects :116-129, resize_by_factor
+    :166-171, paste_over's clipping :131-163): [] when the view is not
+    occluded, else a list of (occluder, w1, h1, x0, y0, x1, y1, sx0, sy0)."""
+    if not np.random.uniform(0, 1) < aug_rate:
+        return []
+    out = []
+    count = np.random.randint(1, num_occluder)
+    for _ in range(count):
+        o = random.choice(range(len(sizes)))                               # random.choice(self.occluders)
+        f = np.random.uniform(0.2, 0.8)
+        h, w = sizes[o]
+        w1, h1 = (int(v) for v in np.round(np.array([w, h]) * f).astype(int))
+        r = paste_rect(np.random.uniform([0, 0], [W, H]), w1, h1, W, H)
+        if r is not None:
+            out.append((o, w1, h1) + r)
+    return out
+
+
+def paste_rect(center, w1, h1, W, H):
+    """paste_over's geometry (utils/udaap/utils_augment.py:146-157): the
+    destination rectangle (x0, y0, x1, y1) and the source start (sx0, sy0) of a
+    w1 x h1 occluder centred at round(center) in a W x H image; None if nothing
+    lands inside."""
+    center = np.round(center).astype(np.int32)
+    wh = np.array([w1, h1])
+    raw0 = center - wh // 2
+    raw1 = raw0 + wh
+    d0 = np.clip(raw0, 0, [W, H])
+    d1 = np.clip(raw1, 0, [W, H])
+    s0 = d0 - raw0
+    if w1 <= 0 or h1 <= 0 or not (d1 > d0).all():
+        return None
+    return int(d0[0]), int(d0[1]), int(d1[0]), int(d1[1]), int(s0[0]), int(s0[1])
+
+
 class DeviceAugment:
     """imgs: uint8 BGR [N,H,W,3] (numpy or device tensor); means: RGB-ordered
     channel means (MouseData.getSemiData)."""
@@ -174,15 +296,22 @@ class DeviceAugment:
     def _draw(self, kps):
         return draw_view(kps, self.W, self.H, self.res, self.sf, self.rf, self.use_flip, self.use_noise)
 
-    def views(self, idx, kps):
-        """idx: source image per view [V]; kps: numpy [V,K,3] pixel keypoints.
+    def views(self, idx, kps, occlusion=None, occ_rate=0.5, num_occluder=8):
+        """idx: source image per view [V]; kps: numpy [V,K,3] pixel keypoints;
+        occlusion: an OcclusionBank (DS_mds useOcclusion, datasets/dataset_mds.py:
+        104-109: drawn after each view's affine, as the loader does).
         -> (images [V,3,res,res] on the device, keypoints [V,K,3] on the device)."""
         mats, noises, out_k = [], [], []
-        for k in kps:
+        pastes, first = [], [0]
+        for v, k in enumerate(kps):
             m, n, kk = self._draw(np.asarray(k, np.float32))
             mats.append(m)
             noises.append(n)
             out_k.append(kk)
+            if occlusion is not None:
+                pastes += [(v,) + p for p in draw_occlusion(self.res, self.res, occlusion.sizes, occ_rate,
+                                                            num_occluder)]
+                first.append(len(pastes))
         V = len(idx)
         idx = np.asarray(idx, np.int32)
         if idx.min() < 0 or idx.max() >= self.N:
@@ -192,4 +321,8 @@ class DeviceAugment:
         noise = torch.tensor(np.array(noises, np.float32), device=self.dev)
         out = torch.empty((V, 3, self.res, self.res), device=self.dev)
         Kn.augment_warp(self.imgs, src, mat, noise, self.img_mean, self.chan_mean, out)
+        if occlusion is not None and pastes:
+            pt = np.array([p[:8] + (p[8] | (p[9] << 16),) for p in pastes], np.int32)
+            Kn.occlude(out, occlusion.bank, occlusion.off, occlusion.hw, torch.from_numpy(pt).to(self.dev),
+                       torch.tensor(first, dtype=torch.int32, device=self.dev), self.chan_mean)
         return out, torch.tensor(np.array(out_k, np.float32), device=self.dev)

@@ -660,3 +660,21 @@ def augment_warp(imgs, src_idx, mat, noise, img_mean, chan_mean, out):
     call("ubpl_augment_warp", _p(imgs), imgs.shape[1], imgs.shape[2], _p(src_idx), _p(mat), _p(noise),
          _p(img_mean), _p(chan_mean), V, Ho, Wo, _p(out))
     return out
+
+
+def occlude(out, bank, off, hw, pastes, view_first, chan_mean):
+    """Random occlusion pastes onto augmented views in place (see augment.hip
+    occlude_kernel): out [V,3,H,W]; bank / off / hw: the occluder bank;
+    pastes int32 [P,9] sorted by view; view_first int32 [V+1]."""
+    _chk(out, "out")
+    _chk(bank, "bank")
+    _chk(off, "off", torch.int64)
+    _chk(hw, "hw", torch.int32)
+    _chk(pastes, "pastes", torch.int32)
+    _chk(view_first, "view_first", torch.int32)
+    _chk(chan_mean, "chan_mean")
+    V, _, H, W = out.shape
+    if view_first.numel() != V + 1 or (pastes.numel() and pastes.shape[-1] != 9):
+        raise ValueError("occlude: paste table does not match %d views" % V)
+    call("ubpl_occlude", _p(out), V, H, W, _p(bank), _p(off), _p(hw), _p(pastes), _p(view_first), _p(chan_mean))
+    return out
