@@ -226,23 +226,43 @@ def pmc_traffic(kind):
 
 
 def pck_record():
-    """PCK@0.2 — the metric's second half — from the real-data harness
-    (tools/mouse_pck.py: the reference's MT_UBPL Mouse experiment, 100 epochs,
-    validate() on the 500-image validation split, all on the HIP path).  It
-    trains for ~4 minutes, so the bench reports the committed record instead
-    of re-training; the decode/PCK path itself is checked bit-exact against
-    the oracle on real images by tests/test_gpu_mouse.py."""
-    p = os.path.join(ROOT, "profiles", "r02_mouse_pck_hg2_e100.json")
+    """PCK@0.2 — the metric's second half — of the real-data harness: the
+    reference's MT_UBPL Mouse experiment (tools/mouse_pck.py: HG2, trainBS 4
+    with 2 labeled, validate() on the 500-image validation split) run on the
+    HIP path for 20 epochs (profiles/r03_mouse_pck_hg2_e20.json), next to the
+    REFERENCE's own train()/validate() on the same epochs, seeds, sampler and
+    augmentation draws (tools/ref_pck.py -> tests/golden/ref_pck.json, CPU, in
+    the build container; tests/test_gpu_mouse.py re-runs the HIP side and checks
+    every validated epoch within 0.1).  It trains for minutes, so the bench
+    reports the committed records instead of re-training; the 100-epoch HIP run
+    is reported beside it (the reference at 100 epochs on CPU would take ~10 h)."""
+    p = os.path.join(ROOT, "profiles", "r03_mouse_pck_hg2_e20.json")
+    r = os.path.join(ROOT, "tests", "golden", "ref_pck.json")
     if not os.path.exists(p):
         return None
     with open(p) as fh:
         d = json.load(fh)
-    return {"value": d["final_pck"][-1], "teachers": d["final_pck"][:-1], "best": d["best_pck"],
-            "epochs": d["config"]["epochs"], "model": d["config"]["model"], "split": d["config"]["split"],
-            "thr": d["config"]["pck_thr"], "source": "profiles/r02_mouse_pck_hg2_e100.json (tools/mouse_pck.py)",
-            "reference_value": None,
-            "note": "mean-of-teachers prediction (projects/MT_UBPL.py:387); the reference publishes no PCK and "
-                    "its Mouse training needs skimage (absent), so the +-0.1 comparison is unpinned"}
+    ref = None
+    if os.path.exists(r):
+        with open(r) as fh:
+            ref = json.load(fh)
+    last = [e for e in d["epochs"] if "pck" in e][-1]
+    rlast = [e for e in ref["epochs"] if "pck" in e][-1] if ref else None
+    out = {"value": last["pck"][-1], "teachers": last["pck"][:-1], "epochs": last["epoch"], "model": d["config"]["model"],
+           "split": d["config"]["split"], "thr": d["config"]["pck_thr"],
+           "source": "profiles/r03_mouse_pck_hg2_e20.json (tools/mouse_pck.py)",
+           "reference_value": rlast["pck"][-1] if rlast and rlast["epoch"] == last["epoch"] else None,
+           "reference_teachers": rlast["pck"][:-1] if rlast and rlast["epoch"] == last["epoch"] else None,
+           "reference_source": "tests/golden/ref_pck.json (tools/ref_pck.py: the reference's train()/validate(), "
+                               "CPU, same seeds / sampler / augmentation draws)",
+           "note": "mean-of-teachers prediction (projects/MT_UBPL.py:387)"}
+    p100 = os.path.join(ROOT, "profiles", "r02_mouse_pck_hg2_e100.json")
+    if os.path.exists(p100):
+        with open(p100) as fh:
+            d100 = json.load(fh)
+        out["hip_100_epochs"] = {"value": d100["final_pck"][-1], "teachers": d100["final_pck"][:-1],
+                                 "source": "profiles/r02_mouse_pck_hg2_e100.json (round-2 augmentation geometry)"}
+    return out
 
 
 def cpu_baseline(steps=1, B=32):

@@ -84,3 +84,37 @@ def test_validate_on_mouse_split_matches_oracle():
         assert np.array_equal(np.array(preds_arr[mi]), np.array(want_preds[mi])), mi
         assert [c.avg for c in acc_c[mi]] == accs[mi], mi
         np.testing.assert_allclose(errs[mi], [c.avg for c in err_c[mi]], rtol=1e-6, atol=1e-6)
+
+
+REF_PCK = os.path.join(ROOT, "tests", "golden", "ref_pck.json")
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.skipif(not (os.path.exists(PACK) and os.path.exists(REF_PCK)),
+                    reason="Mouse pack or reference PCK trajectory missing")
+def test_pck_tracks_the_reference_training():
+    """north_star 'PCK@0.2 within ±0.1 of reference': the MT_UBPL experiment on
+    the Mouse split (HG2, trainBS 4 with 2 labeled, the reference's ramps) run
+    on the HIP path (tools/mouse_pck.py) against the REFERENCE's own train() /
+    validate() run on CPU for the same epochs, seeds, sampler and augmentation
+    draws (tools/ref_pck.py -> tests/golden/ref_pck.json): at every validated
+    epoch, each teacher's PCK@0.2 and the mean-prediction PCK are within 0.1 of
+    the reference's."""
+    import importlib.util
+    import json
+    ref = json.load(open(REF_PCK))
+    epochs = len(ref["epochs"])
+    spec = importlib.util.spec_from_file_location("mouse_pck", os.path.join(ROOT, "tools", "mouse_pck.py"))
+    mp = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mp)
+    log = mp.run(mp.parser().parse_args(["--epochs", str(epochs)]), write=False)
+    checked = 0
+    for r_ref, r in zip(ref["epochs"], log["epochs"]):
+        if "pck" not in r_ref:
+            continue
+        print("epoch %d  ours %s  reference %s" % (r["epoch"], r["pck"], r_ref["pck"]))
+        assert r["epoch"] == r_ref["epoch"]
+        for a, b in zip(r["pck"], r_ref["pck"]):
+            assert abs(a - b) <= 0.1, (r["epoch"], r["pck"], r_ref["pck"])
+        checked += 1
+    assert checked >= 4

@@ -25,7 +25,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
-def main():
+def parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=100)
     ap.add_argument("--model", default="HG2")
@@ -36,7 +36,17 @@ def main():
     ap.add_argument("--no-aug", action="store_true")
     ap.add_argument("--seed", type=int, default=1388)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "mouse_pck.json"))
-    a = ap.parse_args()
+    return ap
+
+
+def main():
+    log = run(parser().parse_args())
+    print(json.dumps({"best_pck": log["best_pck"], "best_epoch": log["best_epoch"], "final_pck": log["final_pck"],
+                      "wall_s": log["wall_s"]}))
+
+
+def run(a, write=True):
+    """The experiment of main() with options `a` (parser() defaults); returns the log."""
 
     from ubpl_amd import _lib, mouse
     from ubpl_amd import parameters as PR
@@ -112,11 +122,11 @@ def main():
     log["best_pck"], log["best_epoch"] = best
     log["final_pck"] = log["epochs"][-1]["pck"]
     log["wall_s"] = round(time.time() - t0, 1)
-    os.makedirs(os.path.dirname(a.out), exist_ok=True)
-    with open(a.out, "w") as f:
-        json.dump(log, f, indent=1)
-    print(json.dumps({"best_pck": best[0], "best_epoch": best[1], "final_pck": log["final_pck"],
-                      "wall_s": log["wall_s"]}))
+    if write:
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(log, f, indent=1)
+    return log
 
 
 if __name__ == "__main__":

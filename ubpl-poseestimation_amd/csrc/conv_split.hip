@@ -694,10 +694,14 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wn = 64 * wid;
     if (PRO) {
-        for (int k = tid; k < K; k += NT) {       // visible after the first barrier of the K loop
+        for (int k = tid; k < K; k += NT) {
             lds_sc[k] = pscale[k];
             lds_sh[k] = pshift[k];
         }
+        // a full barrier (waits for the LDS stores): the K loop's raw s_barrier does
+        // not, and without it a wave could read another wave's coefficients of the
+        // first K step before they land (before any DMA is issued: costs no overlap)
+        __syncthreads();
     }
     const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int by = lam % gridDim.y, bx = lam / gridDim.y;
