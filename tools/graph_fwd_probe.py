@@ -73,9 +73,10 @@ def main():
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     S = int(sys.argv[3]) if len(sys.argv) > 3 else 2
     one = len(sys.argv) > 4 and sys.argv[4] == "1"
-    eager = len(sys.argv) > 5 and sys.argv[5] == "eager"
-    locate = len(sys.argv) > 5 and sys.argv[5] == "locate"
-    trace = len(sys.argv) > 5 and sys.argv[5] == "trace"
+    mode = sys.argv[5] if len(sys.argv) > 5 else ""
+    eager = "eager" in mode              # "eager+locate": the eager forwards, first differing activation named
+    locate = "locate" in mode
+    trace = "trace" in mode
     anchor = [None]
     dev = torch.device("cuda")
     torch.manual_seed(0)

@@ -34,6 +34,12 @@ namespace {
 #ifndef UBPL_SOL_PP
 #define UBPL_SOL_PP 0
 #endif
+#ifndef UBPL_SOL_LB
+#define UBPL_SOL_LB 2
+#endif
+#ifndef UBPL_SOL_LDS_COEF
+#define UBPL_SOL_LDS_COEF 1
+#endif
 
 constexpr int NT = 256;
 constexpr int SOL_PRO_K = 512;   // conv1x1_sol_kernel: largest input channel count with a prologue
@@ -669,7 +675,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 // conv_psa_kernel.  2-stage ring, 2 workgroups per CU.  The activation read is
 // the f32 tensor itself: no split pass, no 6-byte/element PSA image.
 template <int BM, bool PRO, bool EPI = false, int NP = 3, int NS = 2>
-__global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restrict__ x,
+__global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const float* __restrict__ x,
                                                            const uint16_t* __restrict__ wp, int64_t wplane,
                                                            const float* __restrict__ bias,
                                                            const float* __restrict__ pscale,
@@ -693,7 +699,7 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
     const int64_t N = (int64_t)B * P;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wn = 64 * wid;
-    if (PRO) {
+    if (PRO && UBPL_SOL_LDS_COEF) {
         for (int k = tid; k < K; k += NT) {
             lds_sc[k] = pscale[k];
             lds_sh[k] = pshift[k];
@@ -775,7 +781,15 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_sol_kernel(const float* __restr
         const char* base = lds + (t % NS) * (AB + BB);
         // this lane's k half: 8 (scale, shift) pairs
         float sc[8], sh[8];
-        if (PRO) {
+        if (PRO && !UBPL_SOL_LDS_COEF) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float s0 = pscale[kt + e], s1 = pscale[kt + 8 + e];
+                const float h0 = pshift[kt + e], h1 = pshift[kt + 8 + e];
+                sc[e] = h ? s1 : s0;
+                sh[e] = h ? h1 : h0;
+            }
+        } else if (PRO) {
             const float4* qs = reinterpret_cast<const float4*>(lds_sc + kt + 8 * h);
             const float4* qh = reinterpret_cast<const float4*>(lds_sh + kt + 8 * h);
             const float4 s0 = qs[0], s1 = qs[1], h0 = qh[0], h1 = qh[1];
