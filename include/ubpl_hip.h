@@ -252,7 +252,7 @@ int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int
  * both f32 operands (dy [B,Cout,P], x [B,Cin,P], prologue relu(x*pscale +
  * pshift) when pscale != nullptr) split while staged: npieces 3 = 6xbf16,
  * 1 = bf16 operands with f32 accumulation.  _workspace: slab floats,
- * 0 = shape not supported (needs Cin % 128 == 0, Cout % 128 == 0, P % 16 == 0). */
+ * 0 = shape not supported (needs Cin % 64 == 0, Cout % 64 == 0, P % 16 == 0). */
 int64_t ubpl_wgrad1x1_split_load_workspace(int B, int Cin, int Cout, int P);
 /*@ dy:f32[(int64_t)B*Cout*P] x:f32[(int64_t)B*Cin*P] pscale:f32[Cin] pshift:f32[Cin] slab:f32[ubpl_wgrad1x1_split_load_workspace(B,Cin,Cout,P)] dw:f32[(int64_t)Cout*Cin] db:f32[Cout] */
 int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, int Cin, int Cout, int P, const float* pscale,
@@ -281,7 +281,7 @@ int ubpl_stem_weight_s2d_split(const float* w, int Cout, int C, int KS, int npie
  * they are staged (no pre-split image): y = conv(relu(x*pscale + pshift) or x)
  * + bias (+ res, may alias y); wsplit = 3 planes of [Cout][Cin] from
  * ubpl_conv_weights_split (KS = 1); npieces 3 = 6xbf16, 1 = bf16 operands (one
- * plane; no epilogue partials).  Cin % 16 == 0, Cout % 64 == 0, P % 4 == 0.
+ * plane; no epilogue partials).  Cin % 16 == 0, Cout % 16 == 0, P % 4 == 0.
  * stat_part (nullable): BatchNorm partials of y (ubpl_bn_partials layout).
  * _preferred: 1 when the shape is supported and fills the chip. */
 int ubpl_conv1x1_split_load_preferred(int B, int Cin, int Cout, int P);

@@ -244,7 +244,8 @@ def test_bf16_conv1x1_split_load_vs_rounded_f64(case):
         assert e <= 2e-6, e
 
 
-@pytest.mark.parametrize("case", [(2, 256, 128, 64, True), (3, 128, 256, 16, False)])
+@pytest.mark.parametrize("case", [(2, 256, 128, 64, True), (3, 128, 256, 16, False), (2, 64, 128, 32, True),
+                                  (2, 64, 64, 16, False)])
 def test_bf16_wgrad1x1_split_load_vs_rounded_f64(case):
     """1x1 weight gradient with NP = 1 (bf16 operands, f32 accumulation) vs
     float64 of the bf16-rounded operands; the bias gradient sums the f32 dy."""
@@ -386,10 +387,14 @@ def test_conv1x1_split_load_vs_f64(case):
     e32, esp = _rel(y_f32, yref), _rel(y, yref)
     print("sol fwd %s: f32 %.2e split-load %.2e" % (case, e32, esp))
     assert esp <= 2 * e32 + 1e-8, (esp, e32)
-    # without the partials epilogue (the 512-pixel 3-stage kernel where it fills
-    # the chip): the same K order and chunking, so the same bits
+    # without the partials epilogue: the same K order and chunking, so the same
+    # bits — except with a residual, which that kernel adds in its transposed
+    # epilogue instead of seeding the accumulators with it (UBPL_SOL_TEPI)
     y2 = Kn.conv1x1_forward_split_load(d(x32), Kn.conv_weight_split(d(w32), 0, 3), d(b32), ps, ph, res=d(res32))
-    assert torch.equal(y2, y)
+    if resid:
+        assert _rel(y2, yref) <= 2 * e32 + 1e-8, (_rel(y2, yref), e32)
+    else:
+        assert torch.equal(y2, y)
     # BN statistics from the epilogue partials
     gamma, beta = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
     rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
@@ -403,7 +408,7 @@ def test_conv1x1_split_load_vs_f64(case):
     if resid:
         o = d(res32).clone()
         Kn.conv1x1_forward_split_load(d(x32), Kn.conv_weight_split(d(w32), 0, 3), d(b32), ps, ph, res=o, out=o)
-        assert torch.equal(o, y)
+        assert torch.equal(o, y2)
     # data gradient (x = dy, mode-1 weights [Cin][Cout]); Cin plays the output role
     if Cin % 64 == 0:
         dy = torch.randn(B, Cout, H, H, generator=gen)
@@ -415,11 +420,49 @@ def test_conv1x1_split_load_vs_f64(case):
         assert esp <= 2 * e32 + 1e-8, (esp, e32)
 
 
+@pytest.mark.parametrize("case", [(4, 256, 32, 16, False), (8, 256, 16, 16, True), (2, 16, 32, 256, False)])
+def test_conv1x1_split_load_16_channels(case):
+    """The heatmap projection (256 -> K = 16) and its data gradient (K = 16 output
+    channels of the merge_preds dgrad) on conv1x1_sol_kernel: one 64-row tile,
+    rows past Cout clamped on load and never stored; within 2x the f32 path's error."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, H, Cout, pro = case
+    gen = torch.Generator().manual_seed(41 + hash(case) % 1000)
+    x32 = torch.randn(B, Cin, H, H, generator=gen)
+    w32 = torch.randn(Cout, Cin, 1, 1, generator=gen) / np.sqrt(Cin)
+    b32 = torch.randn(Cout, generator=gen)
+    sc32, sh32 = torch.rand(Cin, generator=gen) + 0.5, torch.randn(Cin, generator=gen) * 0.5
+    inp = F.relu(x32.double() * sc32.double()[None, :, None, None] + sh32.double()[None, :, None, None]) if pro \
+        else x32.double()
+    yref = F.conv2d(inp, w32.double(), b32.double())
+    d = lambda t: t.to(DEV)
+    ps, ph = (d(sc32), d(sh32)) if pro else (None, None)
+    assert Kn.conv1x1_split_load_ok(d(x32), Kn.conv_weight_split(d(w32), 0, 3)) or B * H * H < 256 * 256
+    y_f32 = Kn.conv2d_forward(d(x32), d(w32), d(b32), 1, ps, ph)
+    y = Kn.conv1x1_forward_split_load(d(x32), Kn.conv_weight_split(d(w32), 0, 3), d(b32), ps, ph)
+    e32, esp = _rel(y_f32, yref), _rel(y, yref)
+    print("sol16 fwd %s: f32 %.2e split-load %.2e" % (case, e32, esp))
+    assert esp <= 2 * e32 + 1e-8, (esp, e32)
+    dy = torch.randn(B, Cout, H, H, generator=gen)
+    dxref = torch.nn.grad.conv2d_input((B, Cin, H, H), w32.double(), dy.double())
+    dx = Kn.conv1x1_forward_split_load(d(dy), Kn.conv_weight_split(d(w32), 1, 3), None)
+    dx32 = Kn.conv2d_dgrad(d(dy), d(w32))
+    e32, esp = _rel(dx32, dxref), _rel(dx, dxref)
+    print("sol16 dgrad %s: f32 %.2e split-load %.2e" % (case, e32, esp))
+    assert esp <= 2 * e32 + 1e-8, (esp, e32)
+
+
 @pytest.mark.parametrize("case", [(2, 256, 128, 64, True), (2, 128, 256, 32, True), (3, 256, 256, 16, False),
-                                  (4, 128, 128, 4, True)])
+                                  (4, 128, 128, 4, True), (2, 64, 64, 32, True), (2, 64, 128, 32, False),
+                                  (3, 128, 64, 16, True), (2, 64, 64, 128, True)])
 def test_wgrad1x1_split_load_vs_f64(case):
     """1x1 weight + bias gradient with both operands split on load, within 2x
-    the exact-f32 kernel's error against float64; accumulate adds."""
+    the exact-f32 kernel's error against float64 or 8 f32 unit roundoffs
+    (2^-21), whichever is larger; accumulate adds.  The floor: the split path's
+    relative error on random data is ~6 u whatever K (each 16-pixel chunk's
+    MFMA sum is rounded once at the chunk's magnitude, the chunks' errors add
+    at random sign), while the exact-f32 kernel's short split-K fmaf chains
+    reach ~2.5 u at K = 32k pixels (the 64-channel convs at 128x128: K = B*16384)."""
     from ubpl_amd import kernels as Kn
     B, Cin, Cout, H, pro = case
     gen = torch.Generator().manual_seed(17 + hash(case) % 1000)
@@ -440,7 +483,7 @@ def test_wgrad1x1_split_load_vs_f64(case):
     Kn.conv2d_wgrad(d(dy), d(x), 1, 1, dw32, db32, ps, ph, accumulate=False)
     e32, esp = _rel(dw32, dwref), _rel(dw - 0.25, dwref)
     print("wgrad1 %s: f32 %.2e split-load %.2e" % (case, e32, esp))
-    assert esp <= 2 * e32 + 1e-8, (esp, e32)
+    assert esp <= max(2 * e32 + 1e-8, 2.0 ** -21), (esp, e32)
     assert _rel(db + 0.5, dbref) <= 1e-5
 
 

@@ -100,7 +100,7 @@ struct StatsOut {
 template <int U, typename F>
 __device__ __forceinline__ void visit_chan4(int b0, int b1, int C, int c, int hw4, F&& f) {
     const int kq = hw4 >> 8;
-    if ((hw4 & 255) == 0 && (kq & (kq - 1)) == 0) {
+    if (kq > 0 && (hw4 & 255) == 0 && (kq & (kq - 1)) == 0) {
         const int ksh = __builtin_ctz(kq);
         const int nj = (b1 - b0) << ksh;
         const int64_t bstride = (int64_t)C * hw4;

@@ -877,13 +877,16 @@ __global__ void __launch_bounds__(NT, 4) conv_wgrad2_kernel(const float* __restr
 // slab columns are tap-major (n = tap*Cin + ci); dw is the reference layout
 // [Cout][Cin][KS][KS] (ci*KS*KS + tap).  R split-lanes per output element
 // (256/R elements per block) sum interleaved splits with two accumulators;
-// the R partials are combined in a fixed order (deterministic).
+// the R partials are combined in a fixed order (deterministic).  The sums are
+// f64, rounded once: with hundreds of splits (the 1x1 weight gradients over
+// 128x128 planes: K = B*16384 pixels in 8-step slices) an f32 sum of the
+// partials would add more rounding than the slices themselves carry.
 template <int R>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Cout,
                                                           int Cin, int T, int with_bias, float* __restrict__ dw,
                                                           float* __restrict__ db, int accumulate) {
     constexpr int C = 256 / R;
-    __shared__ float red[R][C];
+    __shared__ double red[R][C];
     const int Ntot = Cin * T;
     const int Nt = Ntot + 1;
     const int64_t total = (int64_t)Cout * Nt;
@@ -891,24 +894,25 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     for (int64_t i0 = (int64_t)blockIdx.x * C; i0 < total; i0 += (int64_t)gridDim.x * C) {
         const int64_t i = i0 + c;
         const int64_t ic = i < total ? i : total - 1;
-        float s0 = 0.f, s1 = 0.f;
+        double s0 = 0.0, s1 = 0.0;
         int z = r;
         for (; z + R < splits; z += 2 * R) {
-            s0 += slab[(int64_t)z * total + ic];
-            s1 += slab[(int64_t)(z + R) * total + ic];
+            s0 += (double)slab[(int64_t)z * total + ic];
+            s1 += (double)slab[(int64_t)(z + R) * total + ic];
         }
-        if (z < splits) s0 += slab[(int64_t)z * total + ic];
-        float s = s0 + s1;
+        if (z < splits) s0 += (double)slab[(int64_t)z * total + ic];
+        double sd = s0 + s1;
         if (R > 1) {
-            red[r][c] = s;
+            red[r][c] = sd;
             __syncthreads();
             if (r == 0) {
-                s = red[0][c];
+                sd = red[0][c];
 #pragma unroll
-                for (int q = 1; q < R; ++q) s += red[q][c];
+                for (int q = 1; q < R; ++q) sd += red[q][c];
             }
             __syncthreads();
         }
+        const float s = (float)sd;
         if (r != 0 || i >= total) continue;
         const int m = (int)(i / Nt), n = (int)(i - (int64_t)m * Nt);
         if (n < Ntot) {

@@ -31,6 +31,37 @@ namespace {
 #ifndef UBPL_PSA_PP
 #define UBPL_PSA_PP 1
 #endif
+#ifndef UBPL_PSA_PRIO
+#define UBPL_PSA_PRIO 0
+#endif
+// timing-only diagnostics (wrong or less exact results): no chunked accumulation / no K-step barrier
+#ifndef UBPL_PSA_NOCHUNK
+#define UBPL_PSA_NOCHUNK 0
+#endif
+#ifndef UBPL_PSA_NOWAIT
+#define UBPL_PSA_NOWAIT 0
+#endif
+#ifndef UBPL_PSA_NOSTORE
+#define UBPL_PSA_NOSTORE 0
+#endif
+#ifndef UBPL_SOL_NOSTORE
+#define UBPL_SOL_NOSTORE 0
+#endif
+#ifndef UBPL_SOL_TEPI
+#define UBPL_SOL_TEPI 1
+#endif
+#ifndef UBPL_PSA_NOBAR
+#define UBPL_PSA_NOBAR 0
+#endif
+#ifndef UBPL_SOL_NOCHUNK
+#define UBPL_SOL_NOCHUNK 0
+#endif
+#ifndef UBPL_SOL_NOSPLIT
+#define UBPL_SOL_NOSPLIT 0
+#endif
+#ifndef UBPL_PSA_DMA_IL
+#define UBPL_PSA_DMA_IL 0
+#endif
 #ifndef UBPL_SOL_PP
 #define UBPL_SOL_PP 0
 #endif
@@ -469,7 +500,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
     // DMA lane geometry
     const int lr = lane >> 1;
     const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
-    const bool a_issue = wid < BM / 32;
+    const bool a_issue = BM / 32 >= NT / 64 || wid < BM / 32;   // every wave when BM >= 128
     // per-lane 32-bit byte offsets over wave-uniform bases (scalar + vector
     // addressing: no 64-bit VALU per DMA instruction)
     const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, Cout - 1) * Ktot + 8 * lchunk) * 2);
@@ -484,25 +515,32 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
         b_lane[q] =
             (uint32_t)(((((int64_t)b * G * Hp + oh + pad - PADK) * Wp + ow + pad - PADK) * 16 + 8 * lchunk) * 2);
     }
-    auto stage = [&](int buf, int kt) {
+    // DMA piece d (0 .. NP*(1+BQ)-1) of stage (buf, kt): d = p*(1+BQ) + 0 -> A piece p,
+    // d = p*(1+BQ) + 1 + q -> B piece p, row block q
+    constexpr int NDMA = NP * (1 + BQ);
+    auto stage_piece = [&](int buf, int kt, int d) {
         const int kg = kt >> 4;
         const int tap = kg % T, cg = kg / T;
         const int kh = tap / KS, kw = tap - kh * KS;
         const int64_t boff = ((int64_t)cg * Hp + kh) * Wp * 16 + kw * 16;
         char* base = lds + buf * (AB + BB);
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
+        const int p = d / (1 + BQ), r = d % (1 + BQ);
+        if (r == 0) {
             const char* ab = reinterpret_cast<const char*>(wp + p * wplane + kt);
-            const char* bb = reinterpret_cast<const char*>(xs + p * xplane + boff);
             if (a_issue)
                 __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane),
                                                  (lds_ptr_t)(base + p * BM * 32 + wid * 1024), 16, 0, 0);
-#pragma unroll
-            for (int q = 0; q < BQ; ++q)
-                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane[q]),
-                                                 (lds_ptr_t)(base + AB + p * BNT * 32 + (BQ * wid + q) * 1024), 16,
-                                                 0, 0);
+        } else {
+            const int q = r - 1;
+            const char* bb = reinterpret_cast<const char*>(xs + p * xplane + boff);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane[q]),
+                                             (lds_ptr_t)(base + AB + p * BNT * 32 + (BQ * wid + q) * 1024), 16, 0,
+                                             0);
         }
+    };
+    auto stage = [&](int buf, int kt) {
+#pragma unroll
+        for (int d = 0; d < NDMA; ++d) stage_piece(buf, kt, d);
     };
 
     // accumulators start at bias (+ residual): see conv.hip conv_fwd_kernel
@@ -532,11 +570,16 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             if (a_issue) vm_wait<NP + BQ * NP>();
             else vm_wait<BQ * NP>();
         } else {
-            vm_wait<0>();
+            if (!UBPL_PSA_NOWAIT) vm_wait<0>();
         }
-        __builtin_amdgcn_s_barrier();
+        if (!UBPL_PSA_NOBAR) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (t + NS - 1 < nkt) stage((t + NS - 1) % NS, k_begin + (t + NS - 1) * 16);
+        // UBPL_PSA_DMA_IL: the ping-pong body issues the next stage's DMA pieces
+        // between its MFMA chains instead of all of them ahead of the first chain
+        constexpr bool IL = UBPL_PSA_DMA_IL && NP == 3 && TN > 2 && UBPL_PSA_PP;
+        const bool do_stage = t + NS - 1 < nkt;
+        const int sbuf = (t + NS - 1) % NS, skt = k_begin + (t + NS - 1) * 16;
+        if (!IL && do_stage) stage(sbuf, skt);
         const int cur = t % NS;
         const char* base = lds + cur * (AB + BB);
         bf16x8 af[TM][NP], bfr[TN][NP];
@@ -554,21 +597,27 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
             for (int p = 0; p < NP; ++p)
                 af[i][p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
         }
-        if constexpr (NP == 3 && TN > 2 && UBPL_PSA_PP) {
+        if constexpr (NP == 3 && TN > 2 && UBPL_PSA_PP && !UBPL_PSA_NOCHUNK) {
             // ping-pong chunks: tile q's 6-MFMA chain is issued with tile q-1's
             // 16 drain adds between its MFMAs (3 VALU slots per MFMA gap), so the
             // adds hide in the matrix pipe's gaps instead of trailing each chain
 #pragma unroll
             for (int j = 0; j < TN / 2; ++j) read_b(j);
             __builtin_amdgcn_sched_barrier(0);
+            if (UBPL_PSA_PRIO) __builtin_amdgcn_s_setprio(1);
             floatx16 prev = mfma_split0<NP>(af[0], bfr[0]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = TN / 2; j < TN; ++j) read_b(j);
+            constexpr int NQ = TM * TN - 1;   // chains after the first: DMA slots
 #pragma unroll
             for (int q = 1; q < TM * TN; ++q) {
                 const int j = q / TM, i = q % TM, pj = (q - 1) / TM, pi = (q - 1) % TM;
                 const floatx16 cur = mfma_split0<NP>(af[i], bfr[j]);
+                if (IL && do_stage) {
+#pragma unroll
+                    for (int d = q - 1; d < NDMA; d += NQ) stage_piece(sbuf, skt, d);
+                }
                 drain(acc[pi][pj], prev);
 #pragma unroll
                 for (int g = 0; g < 6; ++g) {
@@ -579,7 +628,8 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                 prev = cur;
             }
             drain(acc[TM - 1][TN - 1], prev);
-        } else if constexpr (NP == 3 && TN > 2) {
+            if (UBPL_PSA_PRIO) __builtin_amdgcn_s_setprio(0);
+        } else if constexpr (NP == 3 && TN > 2 && !UBPL_PSA_NOCHUNK) {
             // (no register room for every tile's chunk at once)  The B fragments
             // come in two halves: 18 reads in flight overflow the 4-bit lgkm
             // counter and the compiler then waits for ALL of them before the first
@@ -600,7 +650,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                 for (int i = 0; i < TM; ++i) {
                     drain(acc[i][j], mfma_split0<NP>(af[i], bfr[j]));
                 }
-        } else if constexpr (NP == 3) {
+        } else if constexpr (NP == 3 && !UBPL_PSA_NOCHUNK) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) read_b(j);
             // every tile's chunk chain first, the f32 adds after them (behind a
@@ -656,7 +706,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < Cout) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+                if (m < Cout && (!UBPL_PSA_NOSTORE || acc[i][j][r] == 1234.5f)) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
             }
     }
 }
@@ -717,7 +767,7 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
     // A DMA (as conv_psa_kernel): wave w < BM/32 moves rows 32w..32w+31 of each piece
     const int lr = lane >> 1;
     const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
-    const bool a_issue = wid < BM / 32;
+    const bool a_issue = BM / 32 >= NT / 64 || wid < BM / 32;   // every wave when BM >= 128
     const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, M - 1) * K + 8 * lchunk) * 2);
     // B DMA: wave w moves k rows 4w..4w+3, lane L pixels n0 + 4L .. +3 (P % 4 == 0)
     uint32_t b_lane;
@@ -760,7 +810,14 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
         obase[j] = (int64_t)b * M * P + p;
     }
     floatx16 acc[TM][TN];
-    ubpl::seed_acc<TM, TN>(acc, bias, res, obase, m0, M, P);
+    // UBPL_SOL_TEPI (with a residual): the output tile leaves through LDS as
+    // float4 rows (8 stores per lane per 32-row block instead of 32 scalar
+    // stores) with the residual added there by float4 loads issued ahead of
+    // the stores, instead of seeding the accumulators with 128 scalar loads per
+    // lane before the K loop (128->256 + skip at 64x64 B=32: 101 -> 91 us);
+    // without a residual the scalar epilogue measured faster
+    const bool tepi = UBPL_SOL_TEPI && !EPI && res != nullptr && ((((uintptr_t)y) | (uintptr_t)res) & 15) == 0;
+    ubpl::seed_acc<TM, TN>(acc, bias, tepi ? nullptr : res, obase, m0, M, P);
 
     const int nkt = K >> 4;
     stage(0, 0);
@@ -812,7 +869,9 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 uint32_t o[NP];
-                split2<NP>(v[2 * e], v[2 * e + 1], o);
+                if (UBPL_SOL_NOSPLIT) split2<1>(v[2 * e], v[2 * e + 1], *reinterpret_cast<uint32_t(*)[1]>(o));
+                if (UBPL_SOL_NOSPLIT) for (int p = 1; p < NP; ++p) o[p] = o[0] ^ (uint32_t)p;
+                else split2<NP>(v[2 * e], v[2 * e + 1], o);
 #pragma unroll
                 for (int p = 0; p < NP; ++p) pk[p][e] = o[p];
             }
@@ -871,7 +930,8 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 // per-chunk accumulation (see conv_fwd_split_kernel)
-                drain(acc[i][j], mfma_split0<NP>(af, bfr[j]));
+                if (UBPL_SOL_NOCHUNK) mfma_split<NP>(acc[i][j], af, bfr[j]);
+                else drain(acc[i][j], mfma_split0<NP>(af, bfr[j]));
             }
             // (register budget: one row block's A fragments live at a time)
             __builtin_amdgcn_sched_barrier(0);
@@ -883,6 +943,46 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
 
     if (EPI && stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0, M, n0 + wn, N, stat_part);
     if (EPI && bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0, M, P, n0 + wn, N, bwd);
+    if (tepi) {
+        // every wave is done with the ring (its last reads waited on above); a
+        // wave-private [32 rows][64 + 4 pixels] f32 image per 32-row block
+        __syncthreads();
+        constexpr int RS = 68;
+        static_assert(NS * (AB + BB) >= 4 * 32 * RS * 4, "transposed epilogue image exceeds the ring");
+        float* img = reinterpret_cast<float*>(lds) + wid * 32 * RS;
+        const int rr = lane >> 4, c4 = (lane & 15) * 4;
+        const int64_t n = n0 + wn + c4;   // 4 pixels of one image (P % 4 == 0)
+        const bool ok = n < N;
+        const int64_t b = ok ? n / P : 0;
+        const int64_t ob = b * M * P + (n - b * P);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            // this block's residual rows first (8 loads in flight, ahead of the
+            // stores, which may alias them)
+            float4 q[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int m = m0 + 32 * i + rr + 4 * k;
+                q[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (res != nullptr && ok && m < M) q[k] = *reinterpret_cast<const float4*>(res + ob + (int64_t)m * P);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) img[((r & 3) + 8 * (r >> 2) + 4 * h) * RS + 32 * j + li] = acc[i][j][r];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int row = rr + 4 * k;
+                const int m = m0 + 32 * i + row;
+                float4 v = *reinterpret_cast<const float4*>(img + row * RS + c4);
+                if (ok && m < M) {
+                    v.x += q[k].x; v.y += q[k].y; v.z += q[k].z; v.w += q[k].w;
+                    *reinterpret_cast<float4*>(y + ob + (int64_t)m * P) = v;
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         if (!nok[j]) continue;
@@ -891,7 +991,7 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < M) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+                if (m < M && (!UBPL_SOL_NOSTORE || acc[i][j][r] == 1234.5f)) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
             }
     }
 }
@@ -1264,77 +1364,104 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa64_kernel(const uint16_t* __r
 // that loaded it (thread t: row t/2 of both operands, pixels 8(t&1)..+7), and
 // the pieces go to a double-buffered LDS image [operand][piece][128 rows][32 B]
 // (chunk swizzle c ^ ((row >> 3) & 1), conflict-free ds_read_b128 fragments,
-// conv_psa_kernel's layout).  Tile 128 x 128, wave tile 64 x 64.
-template <bool PRO, int NP = 3>
+// conv_psa_kernel's layout).  Tile CM x CN (128 or 64 channels of dy / of x:
+// the 64-channel convs of the first residual at 128x128), wave tile CM/2 x CN/2.
+// With 64 rows an operand row is loaded by 4 threads (4 pixels each).
+template <bool PRO, int NP = 3, int CM = 128, int CN = 128>
 __global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                           const float* __restrict__ pscale,
                                                           const float* __restrict__ pshift, int B, int Cin, int Cout,
                                                           int P, int steps_per_split, float* __restrict__ slab) {
     // NP = 3: 6xbf16; NP = 1: bf16 operands, f32 accumulation (the "bf16" precision)
-    constexpr int BM = 128, TM = 2, TN = 2;
-    constexpr int PI = BM * 32;   // one piece image: 128 rows x 16 pixels x 2 B
-    constexpr int OB = NP * PI;   // one operand
-    constexpr int SB = 2 * OB;    // one stage: dy pieces, then x pieces
+    constexpr int TM = CM / 64, TN = CN / 64;
+    constexpr int PIA = CM * 32, PIB = CN * 32;   // one piece image: rows x 16 pixels x 2 B
+    constexpr int OA = NP * PIA;                  // dy pieces, then x pieces
+    constexpr int SB = OA + NP * PIB;             // one stage
+    constexpr int TPA = NT / CM, TPB = NT / CN;   // loader threads per row
+    constexpr int PPA = 16 / TPA, PPB = 16 / TPB; // pixels per loader thread (8 or 4)
+    constexpr int FA = PPA / 4, FB = PPB / 4;     // float4s per loader thread
     __shared__ __attribute__((aligned(16))) char lds[2 * SB];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+    const int wm = (wid >> 1) * (CM / 2), wn = (wid & 1) * (CN / 2);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                               gridDim.x * gridDim.y * gridDim.z);
     const int bx = lam % gridDim.x, by = (lam / gridDim.x) % gridDim.y, bz = lam / (gridDim.x * gridDim.y);
-    const int m0 = by * BM, c0 = bx * BM;
+    const int m0 = by * CM, c0 = bx * CN;
     const int psteps = P >> 4;
     const int total = B * psteps;
     const int s_begin = bz * steps_per_split;
     const int s_end = min(total, s_begin + steps_per_split);
     const int nkt = max(0, s_end - s_begin);
 
-    // loader / splitter: row r of both operands, pixels 8*hp .. 8*hp+7 of the step
-    const int r = tid >> 1, hp = tid & 1;
-    const float* arow = dy + (int64_t)(m0 + r) * P + 8 * hp;
-    const float* brow = x + (int64_t)(c0 + r) * P + 8 * hp;
+    // loader / splitter: dy row ra, pixels PPA*qa .. +PPA-1 of the step; x row rb likewise
+    const int ra = tid / TPA, qa = tid % TPA, rb = tid / TPB, qb = tid % TPB;
+    const float* arow = dy + (int64_t)(m0 + ra) * P + PPA * qa;
+    const float* brow = x + (int64_t)(c0 + rb) * P + PPB * qb;
     float sc = 1.f, sh = 0.f;
     if (PRO) {
-        sc = pscale[c0 + r];
-        sh = pshift[c0 + r];
+        sc = pscale[c0 + rb];
+        sh = pshift[c0 + rb];
     }
-    const int wofs = r * 32 + 16 * (hp ^ ((r >> 3) & 1));
-    auto gload = [&](float4 (&a)[2], float4 (&b)[2], int s) {
+    // 16-B chunk (pixels 8c .. 8c+7) swizzled by row, then the 8-B half for 4-pixel loaders
+    const int wofa = ra * 32 + 16 * (((PPA * qa) >> 3) ^ ((ra >> 3) & 1)) + 2 * ((PPA * qa) & 7);
+    const int wofb = rb * 32 + 16 * (((PPB * qb) >> 3) ^ ((rb >> 3) & 1)) + 2 * ((PPB * qb) & 7);
+    auto gload = [&](float4 (&a)[FA], float4 (&b)[FB], int s) {
         const int bb = s / psteps;
         const int p0 = (s - bb * psteps) * 16;
         const float4* a4 = reinterpret_cast<const float4*>(arow + (int64_t)bb * Cout * P + p0);
         const float4* b4 = reinterpret_cast<const float4*>(brow + (int64_t)bb * Cin * P + p0);
-        a[0] = a4[0];
-        a[1] = a4[1];
-        b[0] = b4[0];
-        b[1] = b4[1];
+#pragma unroll
+        for (int f = 0; f < FA; ++f) a[f] = a4[f];
+#pragma unroll
+        for (int f = 0; f < FB; ++f) b[f] = b4[f];
     };
     float bsum = 0.f;
-    auto split_store = [&](int buf, const float4 (&a)[2], const float4 (&b)[2]) {
-        float va[8] = {a[0].x, a[0].y, a[0].z, a[0].w, a[1].x, a[1].y, a[1].z, a[1].w};
-        float vb[8] = {b[0].x, b[0].y, b[0].z, b[0].w, b[1].x, b[1].y, b[1].z, b[1].w};
-        bsum += ((va[0] + va[1]) + (va[2] + va[3])) + ((va[4] + va[5]) + (va[6] + va[7]));
+    auto split_store = [&](int buf, const float4 (&a)[FA], const float4 (&b)[FB]) {
+        float va[PPA], vb[PPB];
+#pragma unroll
+        for (int f = 0; f < FA; ++f) {
+            va[4 * f] = a[f].x, va[4 * f + 1] = a[f].y, va[4 * f + 2] = a[f].z, va[4 * f + 3] = a[f].w;
+        }
+#pragma unroll
+        for (int f = 0; f < FB; ++f) {
+            vb[4 * f] = b[f].x, vb[4 * f + 1] = b[f].y, vb[4 * f + 2] = b[f].z, vb[4 * f + 3] = b[f].w;
+        }
+        if constexpr (PPA == 8)
+            bsum += ((va[0] + va[1]) + (va[2] + va[3])) + ((va[4] + va[5]) + (va[6] + va[7]));
+        else
+            bsum += (va[0] + va[1]) + (va[2] + va[3]);
         if (PRO) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) vb[e] = fmaxf(fmaf(vb[e], sc, sh), 0.f);
+            for (int e = 0; e < PPB; ++e) vb[e] = fmaxf(fmaf(vb[e], sc, sh), 0.f);
         }
-        uint32_t pa[NP][4], pb[NP][4];
+        uint32_t pa[NP][PPA / 2], pb[NP][PPB / 2];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            uint32_t o[NP], q[NP];
+        for (int e = 0; e < PPA / 2; ++e) {
+            uint32_t o[NP];
             split2<NP>(va[2 * e], va[2 * e + 1], o);
-            split2<NP>(vb[2 * e], vb[2 * e + 1], q);
 #pragma unroll
-            for (int p = 0; p < NP; ++p) {
-                pa[p][e] = o[p];
-                pb[p][e] = q[p];
-            }
+            for (int p = 0; p < NP; ++p) pa[p][e] = o[p];
+        }
+#pragma unroll
+        for (int e = 0; e < PPB / 2; ++e) {
+            uint32_t o[NP];
+            split2<NP>(vb[2 * e], vb[2 * e + 1], o);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) pb[p][e] = o[p];
         }
         char* base = lds + buf * SB;
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-            *reinterpret_cast<uint4*>(base + p * PI + wofs) = make_uint4(pa[p][0], pa[p][1], pa[p][2], pa[p][3]);
-            *reinterpret_cast<uint4*>(base + OB + p * PI + wofs) = make_uint4(pb[p][0], pb[p][1], pb[p][2], pb[p][3]);
+            if constexpr (PPA == 8)
+                *reinterpret_cast<uint4*>(base + p * PIA + wofa) = make_uint4(pa[p][0], pa[p][1], pa[p][2], pa[p][3]);
+            else
+                *reinterpret_cast<uint2*>(base + p * PIA + wofa) = make_uint2(pa[p][0], pa[p][1]);
+            if constexpr (PPB == 8)
+                *reinterpret_cast<uint4*>(base + OA + p * PIB + wofb) =
+                    make_uint4(pb[p][0], pb[p][1], pb[p][2], pb[p][3]);
+            else
+                *reinterpret_cast<uint2*>(base + OA + p * PIB + wofb) = make_uint2(pb[p][0], pb[p][1]);
         }
     };
 
@@ -1347,16 +1474,16 @@ __global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restri
             for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
     const int li = lane & 31, h = lane >> 5;
 
-    float4 cA[2], cB[2], nA[2], nB[2];
+    float4 cA[FA], cB[FB], nA[FA], nB[FB];
     if (nkt > 0) gload(cA, cB, s_begin);
     if (nkt > 1) gload(nA, nB, s_begin + 1);
     for (int t = 0; t < nkt; ++t) {
         // buffer t&1 was last read in step t-2, before every wave's step t-1 barrier
         split_store(t & 1, cA, cB);
-        cA[0] = nA[0];
-        cA[1] = nA[1];
-        cB[0] = nB[0];
-        cB[1] = nB[1];
+#pragma unroll
+        for (int f = 0; f < FA; ++f) cA[f] = nA[f];
+#pragma unroll
+        for (int f = 0; f < FB; ++f) cB[f] = nB[f];
         if (t + 2 < nkt) gload(nA, nB, s_begin + t + 2);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -1368,7 +1495,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restri
             const int row = wm + 32 * i + li;
 #pragma unroll
             for (int p = 0; p < NP; ++p)
-                af[i][p] = *reinterpret_cast<const bf16x8*>(base + p * PI + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+                af[i][p] = *reinterpret_cast<const bf16x8*>(base + p * PIA + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -1376,7 +1503,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restri
 #pragma unroll
             for (int p = 0; p < NP; ++p)
                 bfr[j][p] =
-                    *reinterpret_cast<const bf16x8*>(base + OB + p * PI + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+                    *reinterpret_cast<const bf16x8*>(base + OA + p * PIB + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
         }
         if constexpr (NP == 1) {
 #pragma unroll
@@ -1412,9 +1539,10 @@ __global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restri
                 sl[(int64_t)m * Nt + n] = acc[i][j][q];
             }
     }
-    // bias gradient: the two threads of a row hold its two pixel halves
-    const float bt = bsum + __shfl_xor(bsum, 1, 64);
-    if (bx == 0 && hp == 0) sl[(int64_t)(m0 + r) * Nt + Cin] = bt;
+    // bias gradient: the TPA threads of a row (adjacent lanes) hold its pixel chunks
+    float bt = bsum + __shfl_xor(bsum, 1, 64);
+    if constexpr (TPA == 4) bt += __shfl_xor(bt, 2, 64);
+    if (bx == 0 && qa == 0) sl[(int64_t)(m0 + ra) * Nt + Cin] = bt;
 }
 
 // y[b,m,p] = sum_z slab[z][m][b*P+p] + bias[m] (+ res)
@@ -1810,7 +1938,9 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
 // ---- 1x1 with the split on load
 namespace {
 bool sol_supported(int B, int Cin, int Cout, int P) {
-    return B > 0 && P > 0 && Cin % 16 == 0 && Cin > 0 && Cout % 64 == 0 && P % 4 == 0 && (int64_t)B * P >= 4 &&
+    // Cout % 64 != 0 (the 16-channel heatmap projection, preds.*.conv): one
+    // 64-row tile with the rows past Cout clamped on load and never stored
+    return B > 0 && P > 0 && Cin % 16 == 0 && Cin > 0 && Cout % 16 == 0 && P % 4 == 0 && (int64_t)B * P >= 4 &&
            (int64_t)B * Cin * P * 4 < (1LL << 32) && (int64_t)Cout * Cin * 2 < (1LL << 31);
 }
 }  // namespace
@@ -1834,7 +1964,8 @@ static int sol_bm(int64_t N, int Cout) {
 UBPL_API int ubpl_conv1x1_split_load_preferred(int B, int Cin, int Cout, int P) {
     if (!sol_supported(B, Cin, Cout, P)) return 0;
     const int64_t N = (int64_t)B * P;
-    const int64_t wgs = ((N + 255) / 256) * (Cout / sol_bm(N, Cout));
+    const int bm = sol_bm(N, Cout);
+    const int64_t wgs = ((N + 255) / 256) * ((Cout + bm - 1) / bm);
     return wgs >= occ_info().ncu ? 1 : 0;
 }
 
@@ -1858,9 +1989,9 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     const int64_t N = (int64_t)B * P;
     const int bm = sol_bm(N, Cout);
     const ubpl::BnBwdEpi bwd{bn_part ? bn_x : nullptr, bn_coef, bn_relu, bn_part};
-    dim3 grid((unsigned)((N + 255) / 256), (unsigned)(Cout / bm));
+    dim3 grid((unsigned)((N + 255) / 256), (unsigned)((Cout + bm - 1) / bm));
     const bool epi = stat_part != nullptr || bn_part != nullptr;
-    if (epi && npieces == 1) return (int)hipErrorInvalidValue;   // (epilogue partials: 6xbf16 only)
+    if (epi && (npieces == 1 || Cout % 64 != 0)) return (int)hipErrorInvalidValue;   // (epilogue partials: 6xbf16, whole tiles)
     static const bool ns3 = sol_env("UBPL_SOL_NS", 2) == 3;
 #define UBPL_SOL(BM_, PRO_)                                                                                       \
     do {                                                                                                          \
@@ -1950,13 +2081,15 @@ UBPL_API int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t
 
 // ---- 1x1 weight gradient with the split on load
 namespace {
+int wgrad1_cb(int C) { return C % 128 == 0 ? 128 : 64; }
+
 bool wgrad1_sol_supported(int B, int Cin, int Cout, int P) {
-    return B > 0 && Cin % 128 == 0 && Cout % 128 == 0 && P % 16 == 0 && P > 0 &&
+    return B > 0 && Cin % 64 == 0 && Cout % 64 == 0 && P % 16 == 0 && P > 0 &&
            (int64_t)B * Cin * P < (1LL << 31) && (int64_t)B * Cout * P < (1LL << 31);
 }
 
 int wgrad1_sol_splits(int B, int Cin, int Cout, int P) {
-    const int tiles = (Cin / 128) * (Cout / 128);
+    const int tiles = (Cin / wgrad1_cb(Cin)) * (Cout / wgrad1_cb(Cout));
     const int steps = B * (P / 16);
     int s = 512 / tiles;                                    // one round of 2 workgroups per CU
     if (s < 1) s = 1;
@@ -1967,7 +2100,7 @@ int wgrad1_sol_splits(int B, int Cin, int Cout, int P) {
 }  // namespace
 
 // Floats of slab ubpl_wgrad1x1_split_load needs; 0 = shape not supported
-// (Cin % 128, Cout % 128, P % 16): use ubpl_conv2d_wgrad.
+// (Cin % 64, Cout % 64, P % 16): use ubpl_conv2d_wgrad.
 UBPL_API int64_t ubpl_wgrad1x1_split_load_workspace(int B, int Cin, int Cout, int P) {
     if (!wgrad1_sol_supported(B, Cin, Cout, P)) return 0;
     return (int64_t)wgrad1_sol_splits(B, Cin, Cout, P) * Cout * (Cin + 1);
@@ -1987,19 +2120,28 @@ UBPL_API int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, in
     const int splits = wgrad1_sol_splits(B, Cin, Cout, P);
     const int steps = B * (P / 16);
     const int per = (steps + splits - 1) / splits;
-    dim3 grid((unsigned)(Cin / 128), (unsigned)(Cout / 128), (unsigned)splits);
-    if (pscale != nullptr && npieces == 3)
-        hipLaunchKernelGGL((wgrad1_sol_kernel<true>), grid, dim3(NT), 0, st, dy, x, pscale, pshift, B, Cin, Cout, P,
-                           per, slab);
-    else if (npieces == 3)
-        hipLaunchKernelGGL((wgrad1_sol_kernel<false>), grid, dim3(NT), 0, st, dy, x, pscale, pshift, B, Cin, Cout, P,
-                           per, slab);
-    else if (pscale != nullptr)
-        hipLaunchKernelGGL((wgrad1_sol_kernel<true, 1>), grid, dim3(NT), 0, st, dy, x, pscale, pshift, B, Cin, Cout,
-                           P, per, slab);
-    else
-        hipLaunchKernelGGL((wgrad1_sol_kernel<false, 1>), grid, dim3(NT), 0, st, dy, x, pscale, pshift, B, Cin, Cout,
-                           P, per, slab);
+    const int cm = wgrad1_cb(Cout), cn = wgrad1_cb(Cin);
+    dim3 grid((unsigned)(Cin / cn), (unsigned)(Cout / cm), (unsigned)splits);
+#define UBPL_W1(CM_, CN_)                                                                                          \
+    do {                                                                                                           \
+        if (pscale != nullptr && npieces == 3)                                                                     \
+            hipLaunchKernelGGL((wgrad1_sol_kernel<true, 3, CM_, CN_>), grid, dim3(NT), 0, st, dy, x, pscale,       \
+                               pshift, B, Cin, Cout, P, per, slab);                                                \
+        else if (npieces == 3)                                                                                     \
+            hipLaunchKernelGGL((wgrad1_sol_kernel<false, 3, CM_, CN_>), grid, dim3(NT), 0, st, dy, x, pscale,      \
+                               pshift, B, Cin, Cout, P, per, slab);                                                \
+        else if (pscale != nullptr)                                                                                \
+            hipLaunchKernelGGL((wgrad1_sol_kernel<true, 1, CM_, CN_>), grid, dim3(NT), 0, st, dy, x, pscale,       \
+                               pshift, B, Cin, Cout, P, per, slab);                                                \
+        else                                                                                                       \
+            hipLaunchKernelGGL((wgrad1_sol_kernel<false, 1, CM_, CN_>), grid, dim3(NT), 0, st, dy, x, pscale,      \
+                               pshift, B, Cin, Cout, P, per, slab);                                                \
+    } while (0)
+    if (cm == 128 && cn == 128) UBPL_W1(128, 128);
+    else if (cm == 128) UBPL_W1(128, 64);
+    else if (cn == 128) UBPL_W1(64, 128);
+    else UBPL_W1(64, 64);
+#undef UBPL_W1
     UBPL_LAUNCH_CHECK();
     return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 1, db != nullptr, dw, db, accumulate, stream);
 }

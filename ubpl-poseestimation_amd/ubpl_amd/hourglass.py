@@ -274,8 +274,9 @@ class StackedHourglass(nn.Module):
             for name, shape, kind, live in tab:
                 if kind != "cw" or not live or name == stem or not pieces or shape[1 if mode == 0 else 0] % 16:
                     continue
-                # 6xbf16: 3x3 (PSA path) and 1x1 with 64-row output tiles (split on load)
-                if pieces == 3 and not (shape[2] == 3 or (shape[2] == 1 and shape[0 if mode == 0 else 1] % 64 == 0)):
+                # 6xbf16: 3x3 (PSA path) and 1x1 (split on load; outputs of 16 channels and up,
+                # the heatmap projection included)
+                if pieces == 3 and not (shape[2] == 3 or (shape[2] == 1 and shape[0 if mode == 0 else 1] % 16 == 0)):
                     continue
                 s, n, _ = offs[name]
                 T = shape[2] * shape[3]

@@ -232,6 +232,10 @@ class _ModelStreams:
     def on_teacher(self, mi):
         return torch.cuda.stream(self.side[0 if self._one else self.M + mi])
 
+    def stream(self, i):
+        """side stream of network i (students 0..M-1, their teachers M..2M-1)"""
+        return self.side[0 if self._one else i]
+
     def join(self, tensors=()):
         for s in self.side:
             self.main.wait_stream(s)
@@ -240,6 +244,35 @@ class _ModelStreams:
         for t in tensors:                 # produced on a side stream, used on main
             if t is not None and t.is_cuda:
                 t.record_stream(self.main)
+
+
+# Under torch.distributed with per-network streams, each student's gradient
+# all-reduce is enqueued on that student's stream as soon as its backward (both
+# views: its own stream and, for the second view, its teacher's) is enqueued,
+# so RCCL moves student i's gradients while the other networks' backward still
+# runs; UBPL_AR_OVERLAP=0 all-reduces after the join (the round-2 order).
+_AR_OVERLAP = os.environ.get("UBPL_AR_OVERLAP", "1") != "0"
+
+
+def _join_and_allreduce(mstreams, models):
+    """Join the network streams, merge every student's second-view gradients,
+    SUM-all-reduce the students' gradients (projects/MT_UBPL.py:334-336 ->
+    DDP).  Same sums either way: merge, then one all-reduce per student."""
+    if mstreams is not None and _AR_OVERLAP and D.is_dist():
+        M = len(models)
+        for mi, m in enumerate(models):
+            s = mstreams.stream(mi)
+            s.wait_stream(mstreams.stream(M + mi))     # the second-view backward's stream
+            with torch.cuda.stream(s):
+                m.merge_alt_grads()
+                D.allreduce_grads([m])
+        mstreams.join()
+        return
+    if mstreams:
+        mstreams.join()
+    for m in models:
+        m.merge_alt_grads()
+    D.allreduce_grads(models)
 
 
 # AdamW + the EMA teacher update in one pass per model (FlatAdamW.step_and_ema);
@@ -570,11 +603,7 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
         epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[3 * mi + 1]) if use_ep else 0.
         totals.append(pec + mtc + epc + fdc)
     _backward_all(totals)                                     # :334-336
-    if mstreams:
-        mstreams.join()
-    for m in models:
-        m.merge_alt_grads()
-    D.allreduce_grads(models)
+    _join_and_allreduce(mstreams, models)
     _step_and_ema(models, models_ema, optims, args)
     # ---- records: one device->host copy
     g_rec = []
@@ -764,11 +793,7 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
                 epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else 0.
                 totals.append(pec + mtc + epc + fdc)
             _backward_all(totals)                                     # DualPose_UBPL.py:277-279
-            if mstreams:
-                mstreams.join()
-            for m in models:
-                m.merge_alt_grads()
-            D.allreduce_grads(models)
+            _join_and_allreduce(mstreams, models)
             _step_and_ema(models, models_ema, optims, args)
             g_rec = []
             for mi in range(M):
