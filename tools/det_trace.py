@@ -99,15 +99,18 @@ def main():
         diff = False
         for st, seq in ref.items():
             cs = cur.get(st, [])
+            shown = 0
             for i, (a, b) in enumerate(zip(seq, cs)):
                 if a[0] != b[0] or a[3] != b[3]:
                     diff = True
-                    print("run %d: %-9s first differing op #%d of %d: %s [%d] %s" % (
-                        r, label(st), i, len(seq), a[0], a[1], a[2]), flush=True)
-                    for k in range(max(0, i - 4), min(len(seq), i + 3)) if not ONLY else [i]:
+                    print("run %d: %-9s %s differing op #%d of %d: %s [%d] %s" % (
+                        r, label(st), "first" if not shown else "next", i, len(seq), a[0], a[1], a[2]), flush=True)
+                    lo = max(0, i - (6 if not shown else 0))
+                    for k in range(lo, min(len(seq), i + 1)):
                         print("      #%d %s [%d] %s  ref %s  cur %s" % (k, seq[k][0], seq[k][1], seq[k][2],
                                                                     seq[k][4], cs[k][4] if k < len(cs) else None))
-                    if not ONLY:
+                    shown += 1
+                    if not ONLY or shown >= 4:
                         break
             if len(seq) != len(cs):
                 print("run %d: %s op count %d vs %d" % (r, label(st), len(seq), len(cs)), flush=True)
