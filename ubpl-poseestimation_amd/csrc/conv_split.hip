@@ -47,6 +47,10 @@ namespace {
 #ifndef UBPL_SOL_NOSTORE
 #define UBPL_SOL_NOSTORE 0
 #endif
+// diagnostic: the 1x1 split-load kernel's scalar-epilogue stores as non-temporal stores
+#ifndef UBPL_SOL_NT_STORE
+#define UBPL_SOL_NT_STORE 0
+#endif
 #ifndef UBPL_SOL_TEPI
 #define UBPL_SOL_TEPI 1
 #endif
@@ -991,7 +995,10 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < M && (!UBPL_SOL_NOSTORE || acc[i][j][r] == 1234.5f)) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+                if (m < M && (!UBPL_SOL_NOSTORE || acc[i][j][r] == 1234.5f)) {
+                    if (UBPL_SOL_NT_STORE) __builtin_nontemporal_store(acc[i][j][r], y + obase[j] + (int64_t)m * P);
+                    else y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+                }
             }
     }
 }
