@@ -229,14 +229,17 @@ def pck_record():
     """PCK@0.2 — the metric's second half — of the real-data harness: the
     reference's MT_UBPL Mouse experiment (tools/mouse_pck.py: HG2, trainBS 4
     with 2 labeled, validate() on the 500-image validation split) run on the
-    HIP path for 20 epochs (profiles/r03_mouse_pck_hg2_e20.json), next to the
+    HIP path for 20 epochs (profiles/r0N_mouse_pck_hg2_e20.json), next to the
     REFERENCE's own train()/validate() on the same epochs, seeds, sampler and
     augmentation draws (tools/ref_pck.py -> tests/golden/ref_pck.json, CPU, in
     the build container; tests/test_gpu_mouse.py re-runs the HIP side and checks
     every validated epoch within 0.1).  It trains for minutes, so the bench
     reports the committed records instead of re-training; the 100-epoch HIP run
     is reported beside it (the reference at 100 epochs on CPU would take ~10 h)."""
-    p = os.path.join(ROOT, "profiles", "r03_mouse_pck_hg2_e20.json")
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*_mouse_pck_hg2_e20.json")))
+    # (the newest round's 20-epoch record; without one, round 2's 100-epoch run, no reference beside it)
+    p = found[-1] if found else os.path.join(ROOT, "profiles", "r02_mouse_pck_hg2_e100.json")
     r = os.path.join(ROOT, "tests", "golden", "ref_pck.json")
     if not os.path.exists(p):
         return None
@@ -250,7 +253,7 @@ def pck_record():
     rlast = [e for e in ref["epochs"] if "pck" in e][-1] if ref else None
     out = {"value": last["pck"][-1], "teachers": last["pck"][:-1], "epochs": last["epoch"], "model": d["config"]["model"],
            "split": d["config"]["split"], "thr": d["config"]["pck_thr"],
-           "source": "profiles/r03_mouse_pck_hg2_e20.json (tools/mouse_pck.py)",
+           "source": "%s (tools/mouse_pck.py)" % os.path.relpath(p, ROOT),
            "reference_value": rlast["pck"][-1] if rlast and rlast["epoch"] == last["epoch"] else None,
            "reference_teachers": rlast["pck"][:-1] if rlast and rlast["epoch"] == last["epoch"] else None,
            "reference_source": "tests/golden/ref_pck.json (tools/ref_pck.py: the reference's train()/validate(), "

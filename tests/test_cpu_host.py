@@ -316,3 +316,29 @@ def test_occlusion_draws_follow_the_reference_rng_order():
                     ps.append((o, int(w1), int(h1)) + r)
         want.append(ps)
     assert got == want and sum(map(len, got)) > 5
+
+
+def test_occlude_rejects_out_of_range_paste_rows():
+    """kernels.occlude checks every index occlude_kernel derives from a paste
+    row on the host: occluder index, source window inside the
+    resized occluder, destination inside the view, bank extent."""
+    import torch
+    from ubpl_amd import kernels as Kn
+    hw = torch.tensor([[10, 12], [20, 8]], dtype=torch.int32)
+    off = torch.tensor([0, 10 * 12 * 4], dtype=torch.int64)
+    nbank = 10 * 12 * 4 + 20 * 8 * 4
+    # view, occluder, w1, h1, x0, y0, x1, y1, sx0 | sy0 << 16
+    ok = [0, 1, 6, 10, 3, 4, 9, 14, 0]
+    vf = torch.tensor([0, 1, 1], dtype=torch.int32)
+    Kn._occlude_check(2, 32, 32, nbank, off, hw, torch.tensor([ok], dtype=torch.int32), vf)
+    for bad in ([0, 2] + ok[2:],                       # occluder index past the bank
+                ok[:6] + [40, 14, 0],                  # x1 past the view
+                ok[:8] + [1],                          # source window past the resized width
+                ok[:8] + [(1 << 16)]):                 # ... and height
+        with pytest.raises(ValueError):
+            Kn._occlude_check(2, 32, 32, nbank, off, hw, torch.tensor([bad], dtype=torch.int32), vf)
+    with pytest.raises(ValueError):                    # bank shorter than the occluder
+        Kn._occlude_check(2, 32, 32, nbank - 4, off, hw, torch.tensor([ok], dtype=torch.int32), vf)
+    with pytest.raises(ValueError):                    # view_first not a count of the rows
+        Kn._occlude_check(2, 32, 32, nbank, off, hw, torch.tensor([ok], dtype=torch.int32),
+                          torch.tensor([0, 2, 2], dtype=torch.int32))

@@ -8,8 +8,10 @@ bit-exact to the reference by test_oracle_golden), and the per-batch records
 are folded with the reference's AvgCounters weights (bs per keypoint entry,
 bs*k for the mean).  Accuracies are compared bit-exact, errors to 1e-6.
 
-Needs data/mouse_100_500_0.3.npz (tools/pack_mouse.py; git-ignored, travels
-with the tree): skipped where it has not been built.
+Needs data/mouse_100_500_0.3.npz (tools/pack_mouse.py, run by
+__graft_entry__.build() in the build container; git-ignored, travels with the
+tree): a GPU run without it FAILS — the only real-data PCK check must not pass
+by being skipped.
 """
 import os
 import types
@@ -37,8 +39,13 @@ def _teachers(K=9, S=2):
     return ts
 
 
-@pytest.mark.skipif(not os.path.exists(PACK), reason="Mouse pack not built (tools/pack_mouse.py)")
+def _require_pack():
+    assert os.path.exists(PACK), ("Mouse pack %s missing: build it with tools/pack_mouse.py (or "
+                                  "__graft_entry__.build()) where the reference tree exists" % PACK)
+
+
 def test_validate_on_mouse_split_matches_oracle():
+    _require_pack()
     from ubpl_amd import mouse
     from ubpl_amd import train as T
     data = mouse.MouseData.from_pack(PACK)
@@ -90,8 +97,6 @@ REF_PCK = os.path.join(ROOT, "tests", "golden", "ref_pck.json")
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.skipif(not (os.path.exists(PACK) and os.path.exists(REF_PCK)),
-                    reason="Mouse pack or reference PCK trajectory missing")
 def test_pck_tracks_the_reference_training():
     """north_star 'PCK@0.2 within ±0.1 of reference': the MT_UBPL experiment on
     the Mouse split (HG2, trainBS 4 with 2 labeled, the reference's ramps) run
@@ -103,6 +108,7 @@ def test_pck_tracks_the_reference_training():
     import importlib.util
     import json
     ref = json.load(open(REF_PCK))
+    _require_pack()
     epochs = len(ref["epochs"])
     spec = importlib.util.spec_from_file_location("mouse_pck", os.path.join(ROOT, "tools", "mouse_pck.py"))
     mp = importlib.util.module_from_spec(spec)
@@ -118,3 +124,8 @@ def test_pck_tracks_the_reference_training():
             assert abs(a - b) <= 0.1, (r["epoch"], r["pck"], r_ref["pck"])
         checked += 1
     assert checked >= 4
+    # the +-0.1 window alone accepts a run that learned nothing (the reference
+    # starts at 0.05): the last epoch must also reach half the reference's PCK
+    last_ref, last = ref["epochs"][-1], log["epochs"][-1]
+    for a, b in zip(last["pck"], last_ref["pck"]):
+        assert a >= 0.5 * b, (last["epoch"], last["pck"], last_ref["pck"])

@@ -337,13 +337,24 @@ class StackedHourglass(nn.Module):
             self._alt_pending = []
         return self._alt_grads
 
-    def merge_alt_grads(self):
+    def merge_alt_grads(self, release=True):
         """flat_grads += the concurrent pass's gradients (on the current stream,
-        after it has joined that pass's stream)."""
+        after it has joined that pass's stream).  release=False keeps the
+        tensors the backward streams read (upstream gradients, the concurrent
+        pass's saved activations) alive: a caller merging on a side stream
+        releases them with release_backward_refs() after the main stream has
+        joined it — freed earlier, the caching allocator could hand their
+        blocks to main while those kernels still read them."""
         if getattr(self, "_alt_pending", None):
             self.flat_grads.add_(self._alt_grads)
             self._alt_grads.zero_()
+            self._alt_done = self._alt_pending
             self._alt_pending = []
+        if release:
+            self.release_backward_refs()
+
+    def release_backward_refs(self):
+        self._alt_done = []
         self._grad_keep = []
 
     def live_params(self):

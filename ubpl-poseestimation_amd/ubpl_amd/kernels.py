@@ -662,6 +662,33 @@ def augment_warp(imgs, src_idx, mat, noise, img_mean, chan_mean, out):
     return out
 
 
+def _occlude_check(V, H, W, nbank, off, hw, pastes, view_first):
+    """Every index occlude_kernel derives from a paste row stays inside its
+    buffer (host copies of the small tables; occlusion is opt-in)."""
+    if not pastes.numel():
+        return
+    noff = off.numel()
+    pr = pastes.reshape(-1, 9).cpu().numpy().astype("int64")
+    vf = view_first.cpu().numpy().astype("int64")
+    hwh = hw.reshape(-1, 2).cpu().numpy().astype("int64")
+    if vf[0] != 0 or (vf[1:] < vf[:-1]).any() or vf[-1] != len(pr):
+        raise ValueError("occlude: view_first is not a running count of %d paste rows" % len(pr))
+    v, oc, w1, h1, x0, y0, x1, y1 = (pr[:, i] for i in range(8))
+    sx0, sy0 = pr[:, 8] & 0xFFFF, pr[:, 8] >> 16
+    bad = ((v < 0) | (v >= V) | (oc < 0) | (oc >= min(noff, len(hwh))) | (w1 <= 0) | (h1 <= 0)
+           | (x0 < 0) | (y0 < 0) | (x1 > W) | (y1 > H) | (x1 < x0) | (y1 < y0)
+           | (sx0 + (x1 - x0) > w1) | (sy0 + (y1 - y0) > h1))
+    if bad.any():
+        raise ValueError("occlude: paste row %d is out of range for %dx%d views / %d occluders" % (
+            int(bad.nonzero()[0][0]), H, W, noff))
+    h, w = hwh[oc, 0], hwh[oc, 1]
+    if (h <= 0).any() or (w <= 0).any():
+        raise ValueError("occlude: an occluder of the bank has an empty size")
+    offh = off.cpu().numpy().astype("int64")[oc]
+    if (offh < 0).any() or (offh + h * w * 4 > nbank).any():
+        raise ValueError("occlude: an occluder reaches past the end of the bank")
+
+
 def occlude(out, bank, off, hw, pastes, view_first, chan_mean):
     """Random occlusion pastes onto augmented views in place (see augment.hip
     occlude_kernel): out [V,3,H,W]; bank / off / hw: the occluder bank;
@@ -676,5 +703,6 @@ def occlude(out, bank, off, hw, pastes, view_first, chan_mean):
     V, _, H, W = out.shape
     if view_first.numel() != V + 1 or (pastes.numel() and pastes.shape[-1] != 9):
         raise ValueError("occlude: paste table does not match %d views" % V)
+    _occlude_check(V, H, W, bank.numel(), off, hw, pastes, view_first)
     call("ubpl_occlude", _p(out), V, H, W, _p(bank), _p(off), _p(hw), _p(pastes), _p(view_first), _p(chan_mean))
     return out

@@ -264,9 +264,11 @@ def _join_and_allreduce(mstreams, models):
             s = mstreams.stream(mi)
             s.wait_stream(mstreams.stream(M + mi))     # the second-view backward's stream
             with torch.cuda.stream(s):
-                m.merge_alt_grads()
+                m.merge_alt_grads(release=False)
                 D.allreduce_grads([m])
         mstreams.join()
+        for m in models:
+            m.release_backward_refs()
         return
     if mstreams:
         mstreams.join()
@@ -648,6 +650,22 @@ class _LaggedRecords:
         if prev is not None:
             self._run(prev)
 
+    @contextlib.contextmanager
+    def flushing(self):
+        """Flush on exit — also when the loader raised mid-epoch (the last
+        step's records); then an error the flush itself raises (a wait on a
+        step a GPU error left half-done) does not replace the one already
+        propagating."""
+        try:
+            yield self
+        except BaseException:
+            try:
+                self.flush()
+            except Exception:
+                pass
+            raise
+        self.flush()
+
     @staticmethod
     def _run(item):
         host, ev, consume = item
@@ -671,14 +689,12 @@ def train_mt_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
         e.train()
     runner = _StepGraph.get(_mt_ubpl_core, models, models_ema, optims, args)
     lag = _LaggedRecords()
-    try:
+    with lag.flushing():
         for bat, (augs_imgMap, augs_heatmaps, meta) in enumerate(trainLoader):
             packed, meta_h = runner.run((augs_imgMap, augs_heatmaps, meta), dev)
             # the step's one device->host copy, read after the next step is enqueued
             lag.push(packed, lambda host, bat=bat, meta_h=meta_h: _mt_ubpl_records(
                 host, bat, meta_h, M, pec_c, mtc_c, epc_c, fdc_c, args, verbose))
-    finally:
-        lag.flush()          # also when the loader raises mid-epoch: the last step's records
     return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
 
 
@@ -730,7 +746,7 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
     for e in models_ema:
         e.train()
     lag = _LaggedRecords()
-    try:
+    with lag.flushing():
         for bat, (stu_imgMap, stu_heatmap, ema_imgMap, meta) in enumerate(trainLoader):
             for o in optims:
                 o.zero_grad()
@@ -806,8 +822,6 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
             lag.push(packed, lambda host, bat=bat, ncn=len(cn), K=K, use_ep=use_ep, nfd=len(fd): _dualpose_records(
                 host, bat, ncn, K, use_ep, nfd, M, S, pec_c, mtc_c, epc_c, fdc_c, args, verbose))
             del outs, outs_ema, feats, totals
-    finally:
-        lag.flush()          # also when the loader raises mid-epoch
     return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
 
 
