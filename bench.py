@@ -49,6 +49,9 @@ def make_args(B):
 # BASELINE.json configs this bench can run (the driver runs the default, the headline)
 CONFIGS = {
     "mt_ubpl": dict(project="MT_UBPL", S=2, K=16, B=32, res=256, desc="configs[1-2]: MT_UBPL, HG2, 256x256"),
+    "mt_ubpl_hg2_256_bf16": dict(project="MT_UBPL", S=2, K=16, B=32, res=256, precision="bf16",
+                                 desc="configs[1-2]: MT_UBPL, HG2, 256x256, bf16 MFMA path (conv operands bf16, "
+                                      "f32 accumulation; a secondary line beside the fp32-equivalent headline)"),
     "dualpose_hg4": dict(project="DualPose_UBPL", S=4, K=17, B=16, res=256,
                          desc="configs[3]: DualPose_UBPL, dual HG4, K=17, 256x256, B=16/GPU"),
     "mt_ubpl_hg8_384": dict(project="MT_UBPL", S=8, K=16, B=16, res=384,
@@ -92,6 +95,9 @@ ROOF = {
     "mt_ubpl": ((128, 128, 3, 64, 64), 3, SPLIT6_PEAK_TFLOPS,
                 "conv_psa_kernel<128, 3, 3, 256, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; 6xbf16 "
                 "split-f32 MFMA; f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
+    "mt_ubpl_hg2_256_bf16": ((128, 128, 3, 64, 64), 1, 2500.0,
+                             "conv_psa_kernel (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; bf16 operands, "
+                             "f32 accumulation; peak = bf16 dense MFMA)"),
     "dualpose_hg4": ((128, 128, 3, 64, 64), 3, SPLIT6_PEAK_TFLOPS,
                      "conv_psa_kernel<128, 3, 3, 256, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
                      "6xbf16; f32-equivalent FLOP/s, peak = bf16 dense / 6)"),

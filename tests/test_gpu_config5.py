@@ -2,7 +2,8 @@
 (projects/MT_UBPL.py:157-352) with 8-stack hourglasses
 (models/pose/hourglass.py:12-58, nStack=8) at 384x384 input / 96x96 heatmaps,
 B=16, on the "bf16" conv precision (one bf16 piece per conv operand, f32
-accumulation).
+accumulation) — and the headline workload (configs[1-2]: HG2, 256x256, B=32)
+on the same precision, the bench's secondary `mt_ubpl_hg2_256_bf16` line.
 
 Each kernel of the bf16 path is pinned exactly against bf16-rounded operands
 in test_gpu_split.py; a randomly initialised train-mode hourglass amplifies
@@ -34,18 +35,21 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-S, K, B, RES, STEPS = 8, 16, 16, 384, 8
+K, STEPS = 16, 8
+# (stacks, batch, input resolution): configs[4] and the headline's shape
+CONFIG5 = (8, 16, 384)
+HEADLINE = (2, 32, 256)
 MEANS = [0.4920829, 0.4920829, 0.4920829]
 
 
-def _args():
+def _args(S, RES):
     return types.SimpleNamespace(
         nStack=S, pseudoScoreThr=0.95, ensemblePseudoWeight=10.0, consWeight=10.0, poseWeight=10.0,
         FDLWeight=1.0, FDL_label="labeled", FDL_type="covariance", epo=1, ema_decay=0.999, pseudoWeight=1.0,
         outRes=RES // 4, useEnsemblePseudo=True)
 
 
-def _batch(dev):
+def _batch(dev, B, RES):
     """One synthetic batch of the bench's shape (bench.make_batches): U[0,1)
     images minus the Mouse means, integer keypoints, half labeled (unlabeled
     rows first, as TwoStreamBatchSampler orders them)."""
@@ -64,7 +68,7 @@ def _batch(dev):
     return imgs, None, {"kps": kps, "islabeled": [isl.to(dev)]}
 
 
-def _run(precision):
+def _run(precision, S, B, RES):
     from ubpl_amd import train as T
     from ubpl_amd.hourglass import StackedHourglass
     from ubpl_amd.optim import FlatAdamW
@@ -81,8 +85,8 @@ def _run(precision):
         models.append(m)
         emas.append(e)
         optims.append(FlatAdamW(m, lr=2.5e-4, weight_decay=0.0))
-    batch = _batch(dev)
-    args = _args()
+    batch = _batch(dev, B, RES)
+    args = _args(S, RES)
     recs, counts = [], []
     for _ in range(STEPS):
         buf = io.StringIO()
@@ -98,8 +102,18 @@ def _run(precision):
 
 @pytest.mark.timeout(900)
 def test_config5_bf16_step_trains_like_6xbf16():
-    r1, c1, st1, var1 = _run("bf16")
-    r6, c6, st6, _ = _run("6xbf16")
+    _check(*CONFIG5)
+
+
+@pytest.mark.timeout(600)
+def test_headline_bf16_step_trains_like_6xbf16():
+    """HG2 at 256x256, B=32 (the bench's mt_ubpl_hg2_256_bf16 line), same bars."""
+    _check(*HEADLINE)
+
+
+def _check(S, B, RES):
+    r1, c1, st1, var1 = _run("bf16", S, B, RES)
+    r6, c6, st6, _ = _run("6xbf16", S, B, RES)
     print("pec bf16  ", np.round(r1[:, :2], 5).tolist())
     print("pec 6xbf16", np.round(r6[:, :2], 5).tolist())
     assert np.isfinite(r1).all() and np.isfinite(r6).all()
