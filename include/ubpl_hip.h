@@ -334,6 +334,20 @@ int ubpl_image_mean_u8(const uint8_t* imgs, int N, int64_t n_per_image, float* o
 int ubpl_augment_warp(const uint8_t* imgs, int H, int W, const int* src_idx, const float* mat, const float* noise,
                       const float* img_mean, const float* chan_mean, int V, int Ho, int Wo, float* out, void* stream);
 
+/* ubpl_augment_chain: the same views with the reference's TWO resamplings
+ * (utils/augment.py:119-137) instead of one: stage 1, skimage.transform.rotate
+ * (order 1, constant 0) of the integer crop of the flipped, noise-adjusted image
+ * about the padded crop's centre, pad stripped, into inter [V][3][Hm][Wm]
+ * (Hc x Wc used per view); stage 2, skimage.transform.resize to Ho x Wo (order
+ * 1, pixel centres, mirror edges), minus chan_mean[3] -> out [V][3][Ho][Wo].
+ * geo int [V][8] = (src_idx, flip, ul_x, ul_y, Hp, Wp, Hc, Wc): the grown crop
+ * box corner and size, the stripped size (Hp - Hc = Wp - Wc = 2 * pad, Hc <= Hm,
+ * Wc <= Wm); cs [V][2] = (cos, sin) of the angle; noise as ubpl_augment_warp. */
+/*@ imgs:u8[?] geo:i32[8*V] cs:f32[2*V] noise:f32[3*V] img_mean:f32[?] chan_mean:f32[3] inter:f32[(int64_t)V*3*Hm*Wm] out:f32[(int64_t)V*3*Ho*Wo] */
+int ubpl_augment_chain(const uint8_t* imgs, int H, int W, const int* geo, const float* cs, const float* noise,
+                       const float* img_mean, const float* chan_mean, int V, int Hm, int Wm, float* inter, int Ho,
+                       int Wo, float* out, void* stream);
+
 /* Random occlusion of augmented views (utils/udaap/utils_augment.py:21-25,116-163:
  * augment_occlu / occlude_with_objects / resize_by_factor / paste_over), after
  * ubpl_augment_warp: out [V][3][H][W] (colorNorm'ed) gets, in draw order, each

@@ -1,9 +1,11 @@
-"""f1 — device augmentation (augment.hip) against a numpy statement of the
-same map: bilinear sampling of the (flipped, noisy_mean-adjusted) uint8 BGR
-source at the host-built 2x3 matrix, zero outside, minus the channel means.
-skimage (the reference's resize/rotate) is absent here, so parity with the
-reference's pixels is statistical; the keypoint map is pinned
-bit-exact on the CPU (test_cpu_host.py::test_augment_geometry_...)."""
+"""f1 — device augmentation (augment.hip).  The default two-stage path
+(ubpl_augment_chain: the reference's integer crop -> skimage rotate -> skimage
+resize, utils/augment.py:119-137) against oracle/augment_chain.py, the numpy /
+scipy.ndimage restatement of scikit-image 0.20's two functions (skimage itself
+is absent here: that restatement is unpinned against skimage, see its
+header); the single-warp path (ubpl_augment_warp) against a numpy statement of
+its own map.  The keypoint map is pinned bit-exact on the CPU
+(test_cpu_host.py::test_augment_geometry_...)."""
 import random
 
 import numpy as np
@@ -43,7 +45,7 @@ def test_augment_views_match_numpy_statement():
     rs = np.random.RandomState(0)
     imgs = rs.randint(0, 256, (5, 256, 256, 3)).astype(np.uint8)
     means = [0.45, 0.5, 0.55]
-    aug = DeviceAugment(imgs, means, device="cuda")
+    aug = DeviceAugment(imgs, means, device="cuda", two_stage=False)
     random.seed(3)
     torch.manual_seed(3)
     kps = np.zeros((6, 9, 3), np.float32)
@@ -72,10 +74,59 @@ def test_identity_view_is_the_normalised_image():
     rs = np.random.RandomState(1)
     imgs = rs.randint(0, 256, (2, 256, 256, 3)).astype(np.uint8)
     means = [0.4920829] * 3
-    aug = DeviceAugment(imgs, means, sf=0.0, rf=0.0, use_flip=False, use_noise=False, device="cuda")
-    out, _ = aug.views([1, 0], np.zeros((2, 9, 3), np.float32))
-    want = np.transpose(imgs[[1, 0]].astype(np.float32) / 255., (0, 3, 1, 2)) - np.float32(0.4920829)
-    assert np.abs(out.cpu().numpy() - want).max() < 1e-6
+    for two in (True, False):
+        aug = DeviceAugment(imgs, means, sf=0.0, rf=0.0, use_flip=False, use_noise=False, device="cuda",
+                            two_stage=two)
+        out, _ = aug.views([1, 0], np.zeros((2, 9, 3), np.float32))
+        want = np.transpose(imgs[[1, 0]].astype(np.float32) / 255., (0, 3, 1, 2)) - np.float32(0.4920829)
+        assert np.abs(out.cpu().numpy() - want).max() < 1e-6, two
+
+
+def test_two_stage_views_match_the_reference_chain():
+    """Default path: each view equals the reference's own pixel chain (flip ->
+    noisy_mean -> integer crop -> skimage rotate -> strip pad -> skimage resize
+    -> colorNorm) as oracle/augment_chain.py restates it, to f32 rounding of the
+    sample coordinates (crops up to 451 px: ~3e-5 px)."""
+    from oracle import augment_chain as AC
+    from ubpl_amd.augment import DeviceAugment
+    rs = np.random.RandomState(5)
+    # smooth images with sharp edges (a natural image's mix), not white noise
+    yy, xx = np.mgrid[0:256, 0:256]
+    imgs = np.stack([np.stack([(127 + 120 * np.sin(xx / (7.0 + 3 * i + c)) * np.cos(yy / (11.0 + i))
+                                + 60 * ((xx + 2 * yy + 17 * i) % 97 < 40)).clip(0, 255)
+                               for c in range(3)], -1) for i in range(4)]).astype(np.uint8)
+    means = [0.45, 0.5, 0.55]
+    aug = DeviceAugment(imgs, means, device="cuda")
+    kps = np.zeros((8, 9, 3), np.float32)
+    kps[:, :, :2] = rs.randint(20, 236, (8, 9, 2))
+    kps[:, :, 2] = 1
+    idx = [0, 1, 2, 3, 0, 1, 2, 3]
+    random.seed(21)
+    torch.manual_seed(21)
+    draws = [aug._draw_geo(k) for k in kps]
+    random.seed(21)
+    torch.manual_seed(21)
+    out, kout = aug.views(idx, kps)
+    o = out.cpu().numpy()
+    mu = aug.img_mean.cpu().numpy()
+    rotated = 0
+    for v, (_, noise, kk, ((flip, ulx, uly, Hp, Wp, Hc, Wc), (cs, sn))) in enumerate(draws):
+        src = imgs[idx[v]].astype(np.float32) / np.float32(255.)
+        if flip:
+            src = src[:, ::-1]
+        a, b, on = noise
+        if on > 0:
+            src = np.clip(np.float32(a) * (src - np.float32(mu[idx[v]])) + np.float32(mu[idx[v]]) + np.float32(b),
+                          0, 1)
+        pad = (Hp - Hc) // 2
+        rotated += pad > 0
+        angle = float(np.rad2deg(np.arctan2(sn, cs))) if pad else 0.0
+        ref = AC.affine_view(src.astype(np.float64), (ulx, uly), (ulx + Wp, uly + Hp), pad, angle)
+        ref = np.transpose(ref, (2, 0, 1)) - np.array(means)[:, None, None]
+        d = np.abs(o[v] - ref)
+        assert d.max() < 2e-4 and d.mean() < 2e-6, (v, d.max(), d.mean())
+        assert np.array_equal(kout[v].cpu().numpy(), kk)
+    assert rotated >= 4
 
 
 def _area_resize(occ, w1, h1):

@@ -29,7 +29,7 @@ import time
 import types
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "ubpl-poseestimation_amd"), os.path.join(ROOT, "tests", "golden")]
+sys.path[:0] = [os.path.join(ROOT, "ubpl-poseestimation_amd"), os.path.join(ROOT, "tests", "golden"), ROOT]
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -64,8 +64,30 @@ def warp_np(img, m, noise, mu, means, res):
                                                                                                                 None]))
 
 
+def chain_np(img, geo, noise, mu, means, res):
+    """The reference's own pixel path for one view (utils/augment.py:86-137
+    after fliplr and noisy_mean: integer crop, skimage rotate, skimage resize;
+    oracle/augment_chain.py restates scikit-image 0.20), colorNorm'ed — what
+    DS_mds would hand train() (datasets/dataset_mds.py:88-113)."""
+    from oracle import augment_chain as AC
+    (flip, ulx, uly, Hp, Wp, Hc, Wc), (cs, sn) = geo
+    v = img.astype(np.float32) / np.float32(255.)
+    if flip:
+        v = v[:, ::-1]
+    a, b, on = noise
+    if on > 0:
+        v = np.clip(np.float32(a) * (v - np.float32(mu)) + np.float32(mu) + np.float32(b), 0, 1)
+    pad = (Hp - Hc) // 2
+    angle = float(np.rad2deg(np.arctan2(sn, cs))) if pad else 0.0
+    val = AC.affine_view(v.astype(np.float64), (ulx, uly), (ulx + Wp, uly + Hp), pad, angle, (res, res))
+    return torch.from_numpy(np.ascontiguousarray(np.transpose(val, (2, 0, 1)).astype(np.float32)
+                                                 - np.array(means, np.float32)[:, None, None]))
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--pixels", choices=("chain", "warp"), default="chain",
+                    help="chain: the reference's crop -> rotate -> resize (default); warp: one bilinear sample")
     ap.add_argument("--epochs", type=int, default=20)
     ap.add_argument("--valid-every", type=int, default=5)
     ap.add_argument("--threads", type=int, default=8)
@@ -117,8 +139,11 @@ def main():
             for _ in range(2):                                         # view-major, as mouse_pck.py
                 vx, vh, vg = [], [], []
                 for i in idx:
-                    m, noise, kk = draw_view(kps_all[i], W, H, data.inpRes, 0.25, 30.0)
-                    vx.append(warp_np(imgs[i], m, noise, img_mean[i], means, data.inpRes))
+                    m, noise, kk, geo = draw_view(kps_all[i], W, H, data.inpRes, 0.25, 30.0, with_geometry=True)
+                    if a.pixels == "chain":
+                        vx.append(chain_np(imgs[i], geo, noise, img_mean[i], means, data.inpRes))
+                    else:
+                        vx.append(warp_np(imgs[i], m, noise, img_mean[i], means, data.inpRes))
                     hm, kv = R["P"].kps_heatmap(torch.from_numpy(kk), (3, data.inpRes, data.inpRes), data.inpRes,
                                                 data.outRes)
                     vh.append(hm)
@@ -133,7 +158,9 @@ def main():
             yield views, hms, meta
 
     log = {"what": "reference projects/MT_UBPL.py train()/validate() on CPU, Mouse_100_500_0.3, HG2, trainBS 4 "
-                   "(2 labeled), batches from the CPU restatement of the device augmentation (tools/ref_pck.py)",
+                   "(2 labeled), batches from the CPU restatement of the device augmentation (tools/ref_pck.py), "
+                   "pixels: " + ("the reference's crop -> skimage rotate -> skimage resize chain (oracle/augment_chain.py)"
+                                 if a.pixels == "chain" else "one bilinear warp"),
            "threads": a.threads, "seed": a.seed, "epochs": []}
     t0 = time.time()
     for epo in range(a.epochs):

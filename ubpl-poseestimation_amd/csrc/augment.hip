@@ -83,6 +83,96 @@ __global__ void __launch_bounds__(256) augment_warp_kernel(const uint8_t* __rest
     }
 }
 
+// The reference's two resamplings (utils/augment.py:119-137), ubpl_augment_chain.
+// Stage 1 — skimage.transform.rotate (scikit-image 0.20: order 1, mode
+// 'constant' 0, clip) of the padded integer crop, pad stripped: stripped pixel
+// (r, c) is padded pixel (R, C) = (r + pad, c + pad), which samples the padded
+// crop at s = Rot(angle) ((C, R) - ctr) + ctr, ctr = (Wp/2 - 0.5, Hp/2 - 0.5),
+// bilinear between the floor and ceil neighbours; a neighbour outside the
+// padded crop, or inside it but outside the (flipped) image, reads 0.  Bilinear
+// weights are a convex combination, so rotate's clip to the crop's range is
+// the identity.  geo int [V][8] = (src, flip, ul_x, ul_y, Hp, Wp, Hc, Wc),
+// cs [V][2] = (cos, sin) of the angle (1, 0 and pad 0 when it is 0).
+__global__ void __launch_bounds__(256) augment_rotate_kernel(const uint8_t* __restrict__ imgs, int H, int W,
+                                                             const int* __restrict__ geo,
+                                                             const float* __restrict__ cs,
+                                                             const float* __restrict__ noise,
+                                                             const float* __restrict__ img_mean, int Hm, int Wm,
+                                                             float* __restrict__ inter) {
+    const int v = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int* g = geo + 8 * v;
+    const int src = g[0], flip = g[1], ulx = g[2], uly = g[3], Hp = g[4], Wp = g[5], Hc = g[6], Wc = g[7];
+    if (p >= Hc * Wc) return;
+    const int r = p / Wc, c = p - r * Wc;
+    const int pad = (Hp - Hc) >> 1;
+    const float R = (float)(r + pad), C = (float)(c + pad);
+    const float cx = 0.5f * (float)Wp - 0.5f, cy = 0.5f * (float)Hp - 0.5f;
+    const float co = cs[2 * v], si = cs[2 * v + 1];
+    const float sx = co * (C - cx) - si * (R - cy) + cx;
+    const float sy = si * (C - cx) + co * (R - cy) + cy;
+    const float fx = floorf(sx), fy = floorf(sy);
+    const int x0 = (int)fx, y0 = (int)fy, x1 = (int)ceilf(sx), y1 = (int)ceilf(sy);
+    const float dx = sx - fx, dy = sy - fy;
+    const uint8_t* img = imgs + (int64_t)src * H * W * 3;
+    const bool noisy = noise[3 * v + 2] > 0.f;
+    const float a = noise[3 * v], b = noise[3 * v + 1], mu = img_mean[src];
+    // padded-crop pixel (y, x) -> the flipped image's (y + uly, x + ulx); 0 outside either
+    auto px = [&](int y, int x, int ch) -> float {
+        if (x < 0 || x >= Wp || y < 0 || y >= Hp) return 0.f;
+        const int iy = y + uly, ix = x + ulx;
+        return tap(img, H, W, flip ? W - 1 - ix : ix, iy, ch, a, mu, b, noisy);   // (tap: 0 outside)
+    };
+    const int64_t plane = (int64_t)Hm * Wm;
+    float* o = inter + (int64_t)v * 3 * plane + (int64_t)r * Wm + c;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        const float top = (1.f - dx) * px(y0, x0, ch) + dx * px(y0, x1, ch);
+        const float bot = (1.f - dx) * px(y1, x0, ch) + dx * px(y1, x1, ch);
+        o[ch * plane] = (1.f - dy) * top + dy * bot;
+    }
+}
+
+// Stage 2 — skimage.transform.resize of the Hc x Wc stage-1 image to Ho x Wo
+// (scikit-image 0.20: a Gaussian of sigma = max(0, (in/out - 1) / 2) when the
+// axis shrinks, then scipy.ndimage.zoom(order=1, mode='mirror',
+// grid_mode=True), clip).  The loaders' crops are at most 1.25 * 256 = 320
+// pixels: sigma <= 0.125, radius int(4 sigma + 0.5) <= 1 with a neighbour weight
+// exp(-32) = 1.3e-14 — the identity in f32, not applied.  Output pixel (i, j)
+// samples ((j + 0.5) Wc/Wo - 0.5, (i + 0.5) Hc/Ho - 0.5), bilinear, an index
+// past either edge mirrored (-1 -> 1, n -> n - 2); convex weights: clip is the
+// identity.  Minus chan_mean (colorNorm).
+__device__ __forceinline__ int mirror_idx(int i, int n) {
+    if (n == 1) return 0;
+    return i < 0 ? -i : (i >= n ? 2 * (n - 1) - i : i);
+}
+
+__global__ void __launch_bounds__(256) augment_resize_kernel(const float* __restrict__ inter,
+                                                             const int* __restrict__ geo, int Hm, int Wm,
+                                                             const float* __restrict__ chan_mean, int Ho, int Wo,
+                                                             float* __restrict__ out) {
+    const int v = blockIdx.y;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= Ho * Wo) return;
+    const int i = p / Wo, j = p - i * Wo;
+    const int Hc = geo[8 * v + 6], Wc = geo[8 * v + 7];
+    const float sy = ((float)i + 0.5f) * ((float)Hc / (float)Ho) - 0.5f;
+    const float sx = ((float)j + 0.5f) * ((float)Wc / (float)Wo) - 0.5f;
+    const float fy = floorf(sy), fx = floorf(sx);
+    const float wy = sy - fy, wx = sx - fx;
+    const int y0 = mirror_idx((int)fy, Hc), y1 = mirror_idx((int)fy + 1, Hc);
+    const int x0 = mirror_idx((int)fx, Wc), x1 = mirror_idx((int)fx + 1, Wc);
+    const int64_t plane = (int64_t)Hm * Wm;
+    const float* s = inter + (int64_t)v * 3 * plane;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+        const float* q = s + ch * plane;
+        const float top = (1.f - wx) * q[(int64_t)y0 * Wm + x0] + wx * q[(int64_t)y0 * Wm + x1];
+        const float bot = (1.f - wx) * q[(int64_t)y1 * Wm + x0] + wx * q[(int64_t)y1 * Wm + x1];
+        out[((int64_t)v * 3 + ch) * Ho * Wo + p] = (1.f - wy) * top + wy * bot - chan_mean[ch];
+    }
+}
+
 // Random occlusion (utils/udaap/utils_augment.py:21-25,116-163: augment_occlu ->
 // occlude_with_objects -> resize_by_factor + paste_over) on views already in
 // HBM.  An occluder bank: RGBA float [h][w][4] images (values in [0,1]) packed
@@ -158,6 +248,20 @@ UBPL_API int ubpl_occlude(float* out, int V, int H, int W, const float* bank, co
     dim3 grid((H * W + 255) / 256, V);
     hipLaunchKernelGGL(occlude_kernel, grid, dim3(256), 0, (hipStream_t)stream, out, H, W, bank, off, hw, pastes,
                        view_first, chan_mean);
+    UBPL_LAUNCH_CHECK();
+    return 0;
+}
+
+UBPL_API int ubpl_augment_chain(const uint8_t* imgs, int H, int W, const int* geo, const float* cs,
+                               const float* noise, const float* img_mean, const float* chan_mean, int V, int Hm,
+                               int Wm, float* inter, int Ho, int Wo, float* out, void* stream) {
+    if (V <= 0 || Ho <= 0 || Wo <= 0) return V < 0 ? (int)hipErrorInvalidValue : 0;
+    if (Hm <= 0 || Wm <= 0) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(augment_rotate_kernel, dim3((Hm * Wm + 255) / 256, V), dim3(256), 0, (hipStream_t)stream,
+                       imgs, H, W, geo, cs, noise, img_mean, Hm, Wm, inter);
+    UBPL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(augment_resize_kernel, dim3((Ho * Wo + 255) / 256, V), dim3(256), 0, (hipStream_t)stream,
+                       inter, geo, Hm, Wm, chan_mean, Ho, Wo, out);
     UBPL_LAUNCH_CHECK();
     return 0;
 }

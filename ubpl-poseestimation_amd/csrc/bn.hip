@@ -42,9 +42,16 @@ __device__ __forceinline__ double consume(const double* p) {
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// UBPL_BN_ACQREL=1 (diagnostic): the ticket RMW with agent-scope acq_rel ordering
+// (release: the partials' stores complete and the L2 is written back before it;
+// acquire in the last arriver: its L2 lines invalidated before the partials are read)
+#ifndef UBPL_BN_ACQREL
+#define UBPL_BN_ACQREL 0
+#endif
 __device__ __forceinline__ bool last_arriver(unsigned* cnt, unsigned n) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, UBPL_BN_ACQREL ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
     if (old != n - 1) return false;
     __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;

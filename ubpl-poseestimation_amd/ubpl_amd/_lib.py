@@ -85,6 +85,7 @@ SIGNATURES = {
     "ubpl_image_mean_u8": (I, [P, I, L, P, P]),
     "ubpl_augment_warp": (I, [P, I, I, P, P, P, P, P, I, I, I, P, P]),
     "ubpl_occlude": (I, [P, I, I, I, P, P, P, P, P, P, P]),
+    "ubpl_augment_chain": (I, [P, I, I, P, P, P, P, P, I, I, I, P, I, I, P, P]),
 }
 
 _lib = None

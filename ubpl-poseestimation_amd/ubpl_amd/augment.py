@@ -125,7 +125,20 @@ def warp_matrix(center, scale, res, angle, W, flip=False):
     return M[:2]
 
 
-def draw_view(kps, W, H, res_in, sf, rf, use_flip=True, use_noise=True):
+def chain_geometry(center, scale, res, angle, flip):
+    """The per-view table of ubpl_augment_chain (the reference's two
+    resamplings): (flip, ul_x, ul_y, Hp, Wp, Hc, Wc) — the grown integer crop
+    box of affine_image (corner, padded size) and its size after the pad is
+    stripped — and (cos, sin) of the angle in float64 from its float32 value
+    (skimage.transform.rotate's SimilarityTransform)."""
+    ul, br, pad = crop_box(center, scale, res, angle)
+    Hp, Wp = int(br[1] - ul[1]), int(br[0] - ul[0])
+    th = np.deg2rad(float(torch.as_tensor(angle, dtype=F32))) if pad else 0.0
+    return ((int(flip), int(ul[0]), int(ul[1]), Hp, Wp, Hp - 2 * pad, Wp - 2 * pad),
+            (float(np.cos(th)), float(np.sin(th))))
+
+
+def draw_view(kps, W, H, res_in, sf, rf, use_flip=True, use_noise=True, with_geometry=False):
     """One view's random draws (python `random`, then torch's CPU
     generator, in the reference loader's order) and keypoints (numpy [K,3]
     in, [K,3] out), with the loader's types: keypoints float32 tensors,
@@ -155,6 +168,8 @@ def draw_view(kps, W, H, res_in, sf, rf, use_flip=True, use_noise=True):
         if kps[k, 1] > 0:                                             # augment.py:153
             out[k, :2] = torch.from_numpy(transform_point(kps[k, :2], t))
     m = warp_matrix(center, scale, res, angle, W, flip)
+    if with_geometry:
+        return m.reshape(-1), noise, out.numpy(), chain_geometry(center, scale, res, angle, flip)
     return m.reshape(-1), noise, out.numpy()
 
 
@@ -282,9 +297,14 @@ def paste_rect(center, w1, h1, W, H):
 
 class DeviceAugment:
     """imgs: uint8 BGR [N,H,W,3] (numpy or device tensor); means: RGB-ordered
-    channel means (MouseData.getSemiData)."""
+    channel means (MouseData.getSemiData).  two_stage (default): the
+    reference's pixels — skimage rotate, then resize (ubpl_augment_chain);
+    False: one bilinear sample through the composed map (ubpl_augment_warp,
+    the round-2/3 path; its deviation from the chain is in DESIGN.md §1 f1)."""
 
-    def __init__(self, imgs, means, inp_res=256, sf=0.25, rf=30.0, use_flip=True, use_noise=True, device="cuda"):
+    def __init__(self, imgs, means, inp_res=256, sf=0.25, rf=30.0, use_flip=True, use_noise=True, device="cuda",
+                 two_stage=True):
+        self.two_stage = two_stage
         self.imgs = torch.as_tensor(imgs).to(device).contiguous()
         self.N, self.H, self.W = self.imgs.shape[:3]
         self.res = inp_res
@@ -296,15 +316,21 @@ class DeviceAugment:
     def _draw(self, kps):
         return draw_view(kps, self.W, self.H, self.res, self.sf, self.rf, self.use_flip, self.use_noise)
 
+    def _draw_geo(self, kps):
+        return draw_view(kps, self.W, self.H, self.res, self.sf, self.rf, self.use_flip, self.use_noise,
+                         with_geometry=True)
+
     def views(self, idx, kps, occlusion=None, occ_rate=0.5, num_occluder=8):
         """idx: source image per view [V]; kps: numpy [V,K,3] pixel keypoints;
         occlusion: an OcclusionBank (DS_mds useOcclusion, datasets/dataset_mds.py:
         104-109: drawn after each view's affine, as the loader does).
         -> (images [V,3,res,res] on the device, keypoints [V,K,3] on the device)."""
-        mats, noises, out_k = [], [], []
+        mats, noises, out_k, geos, css = [], [], [], [], []
         pastes, first = [], [0]
         for v, k in enumerate(kps):
-            m, n, kk = self._draw(np.asarray(k, np.float32))
+            m, n, kk, (geo, cs) = self._draw_geo(np.asarray(k, np.float32))
+            geos.append((int(idx[v]),) + geo)
+            css.append(cs)
             mats.append(m)
             noises.append(n)
             out_k.append(kk)
@@ -320,7 +346,13 @@ class DeviceAugment:
         mat = torch.tensor(np.array(mats, np.float32), device=self.dev)
         noise = torch.tensor(np.array(noises, np.float32), device=self.dev)
         out = torch.empty((V, 3, self.res, self.res), device=self.dev)
-        Kn.augment_warp(self.imgs, src, mat, noise, self.img_mean, self.chan_mean, out)
+        if self.two_stage:
+            g = np.array(geos, np.int32)
+            Kn.augment_chain(self.imgs, torch.from_numpy(g).to(self.dev),
+                             torch.tensor(np.array(css, np.float32), device=self.dev), noise, self.img_mean,
+                             self.chan_mean, int(g[:, 6].max()), int(g[:, 7].max()), out)
+        else:
+            Kn.augment_warp(self.imgs, src, mat, noise, self.img_mean, self.chan_mean, out)
         if occlusion is not None and pastes:
             pt = np.array([p[:8] + (p[8] | (p[9] << 16),) for p in pastes], np.int32)
             Kn.occlude(out, occlusion.bank, occlusion.off, occlusion.hw, torch.from_numpy(pt).to(self.dev),

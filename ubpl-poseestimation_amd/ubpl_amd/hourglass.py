@@ -50,6 +50,9 @@ _FWD_EPI = os.environ.get("UBPL_FWD_EPI", "0") == "1"
 # diagnostic (tools/graph_fwd_probe.py locate): the hourglass upsample-add out of place, its
 # up1 input saved, so a graph replay's first wrong activation can name up1 or the add
 _UPADD_OOP = os.environ.get("UBPL_UPADD_OOP", "0") == "1"
+# diagnostic (tools/fwd_race.py, forwards only, weights never updated): re-lay out the weights in a
+# model's first forward only
+_RELAYOUT_ONCE = os.environ.get("UBPL_RELAYOUT_ONCE", "0") == "1"
 
 
 # ---------------------------------------------------------------------------
@@ -417,8 +420,10 @@ class StackedHourglass(nn.Module):
         if save:
             self._grad_keep = []     # the last step's upstream gradients (its streams joined since)
         ex = _Exec(self, B, dev, part, train=self.training, save=save)
-        self.relayout_weights(0)
-        self.relayout_weights(1)       # k-major 1x1 weights for conv1x1_forward_kmajor
+        if not (_RELAYOUT_ONCE and getattr(self, "_relaid", False)):
+            self.relayout_weights(0)
+            self.relayout_weights(1)       # k-major 1x1 weights for conv1x1_forward_kmajor
+            self._relaid = True
         if self.training:
             self._nbt.add_(1)
         else:

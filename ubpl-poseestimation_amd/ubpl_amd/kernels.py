@@ -662,6 +662,28 @@ def augment_warp(imgs, src_idx, mat, noise, img_mean, chan_mean, out):
     return out
 
 
+def augment_chain(imgs, geo, cs, noise, img_mean, chan_mean, Hm, Wm, out):
+    """The reference's two resamplings per view (see augment.hip
+    ubpl_augment_chain): geo int32 [V,8] (src, flip, ul_x, ul_y, Hp, Wp, Hc, Wc),
+    cs float32 [V,2] (cos, sin); out [V,3,Ho,Wo].  Stage-1 scratch [V,3,Hm,Wm]."""
+    _chk(imgs, "imgs", torch.uint8)
+    _chk(geo, "geo", torch.int32)
+    for t, n in ((cs, "cs"), (noise, "noise"), (img_mean, "img_mean"), (chan_mean, "chan_mean"), (out, "out")):
+        _chk(t, n)
+    V, _, Ho, Wo = out.shape
+    if geo.numel() != 8 * V or cs.numel() != 2 * V or noise.numel() != 3 * V:
+        raise ValueError("augment_chain: per-view tables do not match %d views" % V)
+    g = geo.reshape(V, 8).cpu() if geo.is_cuda else geo.reshape(V, 8)
+    if (g[:, 6] > Hm).any() or (g[:, 7] > Wm).any() or (g[:, 6] < 1).any() or (g[:, 7] < 1).any() or \
+            (g[:, 0] < 0).any() or (g[:, 0] >= imgs.shape[0]).any():
+        raise ValueError("augment_chain: a view's stripped crop exceeds %dx%d or its source index is out of range"
+                         % (Hm, Wm))
+    inter = torch.empty((V, 3, Hm, Wm), device=out.device, dtype=F32)
+    call("ubpl_augment_chain", _p(imgs), imgs.shape[1], imgs.shape[2], _p(geo), _p(cs), _p(noise), _p(img_mean),
+         _p(chan_mean), V, int(Hm), int(Wm), _p(inter), Ho, Wo, _p(out))
+    return out
+
+
 def _occlude_check(V, H, W, nbank, off, hw, pastes, view_first):
     """Every index occlude_kernel derives from a paste row stays inside its
     buffer (host copies of the small tables; occlusion is opt-in)."""
