@@ -382,10 +382,11 @@ def main():
     warm = [batches[i % 2] for i in range(a.warmup)]
     timed = [batches[i % 2] for i in range(a.steps)]
 
-    # default step: eager launches, one HIP stream per network (the captured
-    # step graph is off with per-network streams: open race, DESIGN.md §6;
-    # UBPL_STEP_GRAPH=1 forces it — then it is captured on the last warm-up
-    # step and the timed steps are replays)
+    # default step (one rank): one HIP stream per network, the whole step
+    # captured in a HIP graph on the last warm-up step and replayed for the
+    # timed steps (the captured launches are the eager step's, bit for bit:
+    # tests/test_gpu_train.py); UBPL_STEP_GRAPH=0: eager launches.  Under
+    # torch.distributed the step stays eager (RCCL calls inside).
     T._StepGraph.WARM = max(1, a.warmup - 1)
     train(warm, models, emas, optims, args, verbose=False)
     torch.cuda.synchronize()

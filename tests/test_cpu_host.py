@@ -409,3 +409,59 @@ def test_augment_chain_kernel_formulas_match_the_skimage_restatement():
             gaps.append(np.abs(AC.single_warp(img, m) - AC.affine_view(img, ul, br, pad, a)).mean())
     # white noise is the worst case for a changed resampling; measured 0.041-0.062 mean here
     assert len(gaps) >= 6 and 0.02 < float(np.mean(gaps)) < 0.1, gaps
+
+
+def _gfx950_code_objects(path):
+    """The gfx950 code objects of a HIP shared library: the clang offload
+    bundles in its .hip_fatbin section (magic, entry count, then per entry
+    offset / size / triple)."""
+    import struct
+    d = open(path, "rb").read()
+    shoff, = struct.unpack_from("<Q", d, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", d, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQ", d, shoff + i * shentsize) for i in range(shnum)]
+    stroff = secs[shstrndx][4]
+    fb = None
+    for name, _, _, _, off, size in secs:
+        if d[stroff + name:d.index(b"\0", stroff + name)] == b".hip_fatbin":
+            fb = d[off:off + size]
+    assert fb is not None, "no .hip_fatbin section in %s" % path
+    magic, pos, out = b"__CLANG_OFFLOAD_BUNDLE__", 0, []
+    while (pos := fb.find(magic, pos)) >= 0:
+        n, = struct.unpack_from("<Q", fb, pos + 24)
+        p = pos + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", fb, p)
+            triple = fb[p + 24:p + 24 + tl].decode()
+            p += 24 + tl
+            if "gfx950" in triple:
+                out.append(fb[pos + off:pos + off + size])
+        pos += len(magic)
+    return out
+
+
+def test_device_code_has_no_packed_fp32_instructions(tmp_path):
+    """The race of rounds 1-3: a packed-FP32 VALU instruction
+    (v_pk_add_f32 with op_sel) produced wrong results for one 16-lane pass when
+    other kernels' matrix work ran beside it from concurrent queues.  The
+    library is built without the packed-FP32 feature (csrc/Makefile NOPK);
+    this checks the built code objects: not one v_pk_{add,mul,fma}_f32."""
+    import subprocess
+    from ubpl_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libubpl_hip.so not built (run __graft_entry__.build())")
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not in this image")
+    cos = _gfx950_code_objects(_lib.LIB_PATH)
+    assert len(cos) >= 9                                  # one per .hip translation unit
+    n_kernels, bad = 0, []
+    for i, co in enumerate(cos):
+        f = tmp_path / ("co%d" % i)
+        f.write_bytes(co)
+        txt = subprocess.run([objdump, "-d", "--mcpu=gfx950", str(f)], capture_output=True, text=True,
+                             check=True).stdout
+        n_kernels += txt.count("s_endpgm")
+        bad += re.findall(r"v_pk_(?:add|mul|fma)_f32[^\n]*", txt)[:3]
+    assert n_kernels > 100
+    assert not bad, bad

@@ -218,10 +218,10 @@ def test_step_graph_replay_matches_eager(monkeypatch):
     _graph_vs_eager(monkeypatch)
 
 
-@pytest.mark.xfail(reason="open race: captured step with per-network streams diverges from eager in ~40 % of "
-                          "runs (DESIGN.md §6); the graph is off by default in that configuration",
-                   strict=False)
 def test_step_graph_with_model_streams_matches_eager(monkeypatch):
+    """The same with one HIP stream per network (the default configuration):
+    rounds 1-3 saw this diverge in ~40 % of runs — the packed-FP32 instruction
+    fault of DESIGN.md §6, fixed in round 4 (csrc/Makefile NOPK)."""
     monkeypatch.setenv("UBPL_MODEL_STREAMS", "1")
     _graph_vs_eager(monkeypatch)
 

@@ -12,7 +12,10 @@ repeat, which (network, view) outputs differ from the first repeat.
          networks: no overlap), FWD_KEEPALL=1 (every tensor an op allocates kept
          alive until the repeat ends: no memory block reused inside a repeat),
          =2 (kept for the whole run: no block ever reused), UBPL_RELAYOUT_ONCE=1
-         (hourglass.py: the weight re-layouts only in each model's first forward)
+         (hourglass.py: the weight re-layouts only in each model's first forward),
+         FWD_LOCATE=1 (forwards that save for backward; every saved activation of
+         every (network, view) compared with the first repeat's, in execution
+         order: names the first layer whose output differs)
 """
 import os
 import sys
@@ -21,6 +24,25 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "ubpl-poseestimation_amd"), ROOT]
 
 import torch  # noqa: E402
+
+
+def analyse_add(r, n, v, k, up, low, out):
+    """out should be up + nearest-upsample(low); name what the wrong elements hold instead."""
+    lu = low.repeat_interleave(2, dim=2).repeat_interleave(2, dim=3)
+    want = up + lu
+    bad = (out != want).reshape(-1)
+    nb = int(bad.sum())
+    if nb == 0:
+        return
+    o, u, w, l2 = out.reshape(-1)[bad], up.reshape(-1)[bad], want.reshape(-1)[bad], lu.reshape(-1)[bad]
+    idx = bad.nonzero().reshape(-1)
+    # 4 floats per thread, 256 threads per block: block-sized chunks of the flat index
+    blk = torch.unique(idx // 1024)
+    print("   rep %d net%d/v%d %s: %d of %d wrong (%.2f%%); =up (add missing) %d, =up+2low (added twice) %d, "
+          "=0 %d; flat index %d..%d, %d distinct 1024-element chunks (first %s)" % (
+              r, n, v, k, nb, bad.numel(), 100.0 * nb / bad.numel(), int((o == u).sum()),
+              int((o == u + 2 * l2).sum()), int((o == 0).sum()), int(idx[0]), int(idx[-1]), blk.numel(),
+              blk[:6].tolist()), flush=True)
 
 
 def main():
@@ -33,6 +55,16 @@ def main():
     from ubpl_amd import _lib
     from ubpl_amd.hourglass import StackedHourglass
     _lib.load()
+    locate = os.environ.get("FWD_LOCATE", "0") == "1"
+    if locate:
+        grad = True
+        orig = StackedHourglass._forward_impl
+
+        def fwd_impl(self, imgs, save):
+            P, F, ex = orig(self, imgs, save)
+            self._last_saved = [(k, v) for k, v in ex.saved.items()]
+            return P, F, ex
+        StackedHourglass._forward_impl = fwd_impl
     dev = torch.device("cuda", 0)
     torch.manual_seed(1388)
     models = [StackedHourglass(16, 2, "AvgPool") for _ in range(nets)]
@@ -67,6 +99,12 @@ def main():
                     with torch.set_grad_enabled(grad):
                         o = models[n](imgs[v])[0]
                     outs[n][v] = o.detach().clone()
+                    if locate:
+                        flat = []
+                        for k, val in models[n]._last_saved:
+                            for i, t in enumerate(val if isinstance(val, tuple) else (val,)):
+                                flat.append(("%s[%d]" % (k, i), t.detach().clone()))
+                        outs[n][v] = (outs[n][v], flat)
             if sync:
                 torch.cuda.synchronize()
         for s in side:
@@ -78,8 +116,29 @@ def main():
     bad = 0
     for r in range(1, reps):
         cur = once()
+        if locate:
+            for n in range(nets):
+                for v in range(views):
+                    shown = 0
+                    cd = dict(cur[n][v][1])
+                    for k, b in cur[n][v][1]:
+                        if k.endswith(".add_out[0]") and k.replace(".add_out[0]", ".add_in[0]") in cd:
+                            analyse_add(r, n, v, k, cd[k.replace(".add_out[0]", ".add_in[0]")],
+                                        cd[k.replace(".add_out[0]", ".add_in[1]")], b)
+                    for (k, a), (_, b) in zip(ref[n][v][1], cur[n][v][1]):
+                        if not torch.equal(a, b):
+                            print("   rep %d net%d/v%d %s differing saved tensor: %s %s max |d| %.3g" % (
+                                r, n, v, "first" if not shown else "next", k, tuple(a.shape),
+                                float((a - b).abs().max())), flush=True)
+                            shown += 1
+                            if shown >= int(os.environ.get("FWD_SHOW", "1")):
+                                break
+            strip = lambda o: [[x[0] for x in row] for row in o]
+            rr, cc = strip(ref), strip(cur)
+        else:
+            rr, cc = ref, cur
         diff = [(n, v, float((a - b).abs().max())) for n in range(nets) for v in range(views)
-                for a, b in [(ref[n][v], cur[n][v])] if not torch.equal(a, b)]
+                for a, b in [(rr[n][v], cc[n][v])] if not torch.equal(a, b)]
         bad += bool(diff)
         print("rep %d: %s" % (r, " ".join("net%d/v%d %.3g" % d for d in diff) or "identical"), flush=True)
     print("fwd_race nets=%d views=%d streams=%d grad=%d sync=%d keep=%s precision=%s: %d of %d repeats differ" % (

@@ -1646,7 +1646,12 @@ Plan fwd_plan(int Cout, int64_t N, int Ktot, int np, bool psa = false) {
     const Occ& d = occ_info();
     const int bk = psa ? 16 : BK;
     const int nkt = (Ktot + bk - 1) / bk;
-    const int maxs = nkt / 2 > 0 ? nkt / 2 : 1;
+    // UBPL_NO_SPLITK=1 (diagnostic): never split K (no slab, no reduce launch)
+    static const bool no_splitk = [] {
+        const char* e = std::getenv("UBPL_NO_SPLITK");
+        return e != nullptr && e[0] == '1';
+    }();
+    const int maxs = no_splitk ? 1 : (nkt / 2 > 0 ? nkt / 2 : 1);
     Plan best{64, 1, 0};
     double bc = 1e30;
     for (int bm : {128, 64}) {

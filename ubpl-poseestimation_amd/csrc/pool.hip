@@ -128,10 +128,17 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const float* __restric
     }
 }
 
+// UBPL_UPADD_FENCE (diagnostic): every upsample-add workgroup starts with an
+// agent-scope acquire fence (its XCD's L2 invalidated before it reads up / low)
+#ifndef UBPL_UPADD_FENCE
+#define UBPL_UPADD_FENCE 0
+#endif
+
 // The same, W % 4 == 0 and 16-B aligned: 4 outputs (one float4 of up / out, one
 // float2 of low) per thread.  total4 = planes*H*W/4.
 __global__ void __launch_bounds__(256) upadd_fwd_vec_kernel(const float* up, const float* __restrict__ low,
                                                            int H, int W, int64_t total4, float* out) {
+    if (UBPL_UPADD_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const int W4 = W >> 2, Wl = W >> 1;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += stride) {
@@ -150,6 +157,7 @@ template <bool STATS>
 __global__ void __launch_bounds__(256) upadd_fwd_kernel(const float* up, const float* __restrict__ low,
                                                        int64_t planes, int H, int W, float* out, int C,
                                                        float* __restrict__ part) {
+    if (UBPL_UPADD_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const int Hl = H >> 1, Wl = W >> 1;
     const int64_t total = planes * H * W;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;

@@ -53,6 +53,9 @@ _UPADD_OOP = os.environ.get("UBPL_UPADD_OOP", "0") == "1"
 # diagnostic (tools/fwd_race.py, forwards only, weights never updated): re-lay out the weights in a
 # model's first forward only
 _RELAYOUT_ONCE = os.environ.get("UBPL_RELAYOUT_ONCE", "0") == "1"
+# diagnostic (tools/fwd_race.py locate): keep low3 (the add's second operand) as a saved activation
+# ("1": the tensor itself, kept alive; "clone": a copy made right after it is produced)
+_SAVE_LOW3 = os.environ.get("UBPL_SAVE_LOW3", "")
 
 
 # ---------------------------------------------------------------------------
@@ -349,7 +352,9 @@ class StackedHourglass(nn.Module):
         joined it — freed earlier, the caching allocator could hand their
         blocks to main while those kernels still read them."""
         if getattr(self, "_alt_pending", None):
-            self.flat_grads.add_(self._alt_grads)
+            # (the library's add: no packed-FP32 instructions, see csrc/Makefile NOPK; this may run on a
+            # side stream beside other networks' backward)
+            Kn.add(self.flat_grads, self._alt_grads, out=self.flat_grads)
             self._alt_grads.zero_()
             self._alt_done = self._alt_pending
             self._alt_pending = []
@@ -665,6 +670,8 @@ class _Exec:
         low1 = self.residual(p + ".low1", pl)
         low2 = self.hourglass(p + ".low2", n - 1, low1) if n > 1 else self.residual(p + ".low2", low1)
         low3 = self.residual(p + ".low3", low2)
+        if _SAVE_LOW3 in ("1", "clone"):                 # diagnostic: the residual's output before the add
+            self.save(p + ".low3_out", low3.clone() if _SAVE_LOW3 == "clone" else low3)
         self.save(p, x)
         part = self.stat_buffer(up1.shape)
         if _UPADD_OOP:                                   # diagnostic: up1 kept, the sum in a new tensor
@@ -672,7 +679,11 @@ class _Exec:
             out = Kn.upsample2x_add(up1, low3, stat_part=part)
             self.give_part(out, part)
             return out
+        if _SAVE_LOW3 == "add":                          # diagnostic: both operands and the result, cloned
+            self.save(p + ".add_in", (up1.clone(), low3.clone()))
         out = Kn.upsample2x_add(up1, low3, out=up1, stat_part=part)
+        if _SAVE_LOW3 == "add":
+            self.save(p + ".add_out", out.clone())
         self.give_part(out, part)
         return out
 

@@ -319,14 +319,28 @@ class _OnMain(torch.autograd.Function):
         return g
 
 
-def _backward_all(totals):
+def _backward_all(totals, outputs=None):
     """The reference runs total_i.backward(retain_graph=True) once per student
     (projects/MT_UBPL.py:334-336): the shared FDL term makes every call reach
     every student, so each network's backward would run M times with gradients
     that are then summed into .grad.  Backward is linear, so one traversal of
     sum_i total_i accumulates the same gradients with each network's backward
-    run once (its upstream gradients summed first)."""
-    torch.autograd.backward(totals)
+    run once (its upstream gradients summed first).
+
+    outputs (the networks' outputs the losses read): two phases — first every
+    loss gradient w.r.t. those outputs, on the main stream, then the networks'
+    backwards from them, on their own streams — so no PyTorch elementwise
+    kernel (autograd's gradient sums, the loss backward) runs beside the
+    networks' matrix work: PyTorch's kernels use packed-FP32 instructions,
+    which this hardware mis-executed beside concurrent matrix work (csrc/Makefile
+    NOPK)."""
+    if outputs is None:
+        torch.autograd.backward(totals)
+        return
+    outs = [t for t in outputs if t is not None and t.requires_grad]
+    grads = torch.autograd.grad(totals, outs, allow_unused=True)
+    pairs = [(t, g) for t, g in zip(outs, grads) if g is not None]
+    torch.autograd.backward([t for t, _ in pairs], [g for _, g in pairs])
 
 
 # ---------------------------------------------------------------------------
@@ -406,18 +420,13 @@ class _StepGraph:
 
     def __init__(self, core, models, models_ema, optims, args):
         self.core, self.models, self.emas, self.optims, self.args = core, models, models_ema, optims, args
-        # default: captured only when the networks share one stream.  With
-        # per-network streams the captured step (and its eager warm-up on a
-        # non-null stream) diverges from the eager step now and then (DESIGN.md
-        # §6, open race); UBPL_STEP_GRAPH=1 forces capture, =0 disables it.
+        # default: captured, with or without per-network streams (rounds 1-3 kept
+        # it off with streams for a divergence whose cause — packed-FP32
+        # instructions beside concurrent matrix work — round 4 removed: DESIGN.md
+        # §6); UBPL_STEP_GRAPH=0 disables it.
         env = os.environ.get("UBPL_STEP_GRAPH")
-        streams = len(models) >= 2 and os.environ.get("UBPL_MODEL_STREAMS", "1") != "0"
-        want = (env == "1") if env is not None else not streams
+        want = env != "0"
         self.enabled = want and not D.is_dist() and all(hasattr(o, "_step_t") for o in optims)
-        if self.enabled and streams:
-            import warnings
-            warnings.warn("ubpl_amd: UBPL_STEP_GRAPH=1 with per-network streams: the captured step is not "
-                          "bit-identical to the eager step (DESIGN.md §6)", RuntimeWarning)
         self.hkey = None
         self.n_eager = 0
         self.graph = None
@@ -604,7 +613,7 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
         pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[3 * mi])
         epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[3 * mi + 1]) if use_ep else 0.
         totals.append(pec + mtc + epc + fdc)
-    _backward_all(totals)                                     # :334-336
+    _backward_all(totals, [t for grp in (outs, feats) for ts in grp for t in ts] if mstreams else None)   # :334-336
     _join_and_allreduce(mstreams, models)
     _step_and_ema(models, models_ema, optims, args)
     # ---- records: one device->host copy
@@ -808,7 +817,7 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
                 pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[6 * mi + 1])
                 epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else 0.
                 totals.append(pec + mtc + epc + fdc)
-            _backward_all(totals)                                     # DualPose_UBPL.py:277-279
+            _backward_all(totals, outs + feats if mstreams else None)   # DualPose_UBPL.py:277-279
             _join_and_allreduce(mstreams, models)
             _step_and_ema(models, models_ema, optims, args)
             g_rec = []
