@@ -22,9 +22,15 @@ def load(path):
         if "conv" not in name:
             continue
         key = name.replace("void (anonymous namespace)::", "").split("(")[0]
+        if BY_GRID:
+            key += " grid=%d" % (int(r["Grid_Size"]) // 256)
         per[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
         dur[key][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     return per, dur
+
+
+# PMC_BY_GRID=1: one entry per (kernel, workgroup count) — the shapes of one template apart
+BY_GRID = os.environ.get("PMC_BY_GRID") == "1"
 
 
 def main():
