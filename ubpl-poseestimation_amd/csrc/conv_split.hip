@@ -77,6 +77,8 @@ namespace {
 #endif
 
 constexpr int NT = 256;
+constexpr bool PSA_WS = false;   // conv_psa_kernel 128 x 256 tiles, 6xbf16: warp-specialized variant (opt-in, measured no gain: DESIGN §6)
+constexpr int PSA_KSUB1 = 2;     // conv_psa_kernel on the bf16 path: 16-k steps per stage (measured)
 constexpr int SOL_PRO_K = 512;   // conv1x1_sol_kernel: largest input channel count with a prologue
 constexpr int BK = 32;
 constexpr int BN = 128;
@@ -468,8 +470,16 @@ __device__ __forceinline__ void vm_wait() {
 // EPI: the opt-in BatchNorm-partials epilogues (UBPL_FWD_EPI / UBPL_BWD_EPI)
 // are compiled in; without them the kernel needs no scratch (the epilogue's
 // register pressure spilled ~190 VGPRs to scratch in every launch).
-template <int BM, int KS, int NP, int BNT = 128, int WGM = 2, bool EPI = false>
-__global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
+// KSUB: 16-k steps per stage and barrier (1; 2-4 on the one-piece bf16 path,
+// whose single MFMA per tile per 16-k step left the loop bound by the ring's
+// barriers and waits: KSUB steps of MFMAs between two barriers)
+// WS (warp-specialized, 512 threads): waves 0-3 compute (the 4-wave tile as
+// below), waves 4-7 only move the operands (the same DMA pieces, one loader per
+// compute wave's share) through a 4-stage ring, 2 K steps ahead; one barrier per
+// K step retires a stage.  A compute wave issues no DMA and waits on no vmcnt:
+// its SIMD partner is the loader, not a second MFMA-dense wave.
+template <int BM, int KS, int NP, int BNT = 128, int WGM = 2, bool EPI = false, int KSUB = 1, bool WS = false>
+__global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
                                                         int B, int Cin, int H, int W, int pad, int Cout, int kchunk,
@@ -484,14 +494,18 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
     constexpr int AB = NP * BM * 32, BB = NP * BNT * 32;   // bytes per stage
     // 128-pixel tiles: 3-stage ring; 256-pixel tiles (wave tile 64 x 128, twice
     // the MFMAs per barrier and per fragment byte): 2 stages, 2 workgroups per CU
-    constexpr int NS = BNT == 256 ? 2 : 3;
+    constexpr int NS = WS ? 4 : (BNT == 256 ? 2 : 3);
+    static_assert(!WS || (BM == 128 && BNT == 256 && KSUB == 1 && !EPI), "warp-specialized: the 128 x 256 tile");
     constexpr int BQ = BNT / 128;                          // B DMA instructions per wave per piece
-    __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
+    constexpr int SB = AB + BB;                            // one 16-k step's image
+    __shared__ __attribute__((aligned(16))) char lds[NS * KSUB * SB];
 
     const int P = H * W, Hp = H + 2 * pad, Wp = W + 2 * pad, G = Cin >> 4;
     const int64_t N = (int64_t)B * P;
     const int Ktot = Cin * T;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool loader = WS && wid >= 4;
+    const int dw = WS ? (wid & 3) : wid;                   // the wave's share of the DMA pieces
     const int wm = (wid / WGN) * (BM / WGM), wn = (wid % WGN) * (BNT / WGN);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                               gridDim.x * gridDim.y * gridDim.z);
@@ -504,14 +518,14 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
     // DMA lane geometry
     const int lr = lane >> 1;
     const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
-    const bool a_issue = BM / 32 >= NT / 64 || wid < BM / 32;   // every wave when BM >= 128
+    const bool a_issue = BM / 32 >= NT / 64 || dw < BM / 32;   // every wave when BM >= 128
     // per-lane 32-bit byte offsets over wave-uniform bases (scalar + vector
     // addressing: no 64-bit VALU per DMA instruction)
-    const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, Cout - 1) * Ktot + 8 * lchunk) * 2);
+    const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * dw + lr, Cout - 1) * Ktot + 8 * lchunk) * 2);
     uint32_t b_lane[BQ];   // wave w moves pixel rows 32*(BQ*w + q) .. +31
 #pragma unroll
     for (int q = 0; q < BQ; ++q) {
-        int64_t n = n0 + 32 * (BQ * wid + q) + lr;
+        int64_t n = n0 + 32 * (BQ * dw + q) + lr;
         n = n < N ? n : N - 1;
         const int b = (int)(n / P);
         const int p = (int)(n - (int64_t)b * P);
@@ -522,30 +536,58 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
     // DMA piece d (0 .. NP*(1+BQ)-1) of stage (buf, kt): d = p*(1+BQ) + 0 -> A piece p,
     // d = p*(1+BQ) + 1 + q -> B piece p, row block q
     constexpr int NDMA = NP * (1 + BQ);
+    // buf: the 16-k step's image slot (stage * KSUB + sub-step)
     auto stage_piece = [&](int buf, int kt, int d) {
         const int kg = kt >> 4;
         const int tap = kg % T, cg = kg / T;
         const int kh = tap / KS, kw = tap - kh * KS;
         const int64_t boff = ((int64_t)cg * Hp + kh) * Wp * 16 + kw * 16;
-        char* base = lds + buf * (AB + BB);
+        char* base = lds + buf * SB;
         const int p = d / (1 + BQ), r = d % (1 + BQ);
         if (r == 0) {
             const char* ab = reinterpret_cast<const char*>(wp + p * wplane + kt);
             if (a_issue)
                 __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane),
-                                                 (lds_ptr_t)(base + p * BM * 32 + wid * 1024), 16, 0, 0);
+                                                 (lds_ptr_t)(base + p * BM * 32 + dw * 1024), 16, 0, 0);
         } else {
             const int q = r - 1;
             const char* bb = reinterpret_cast<const char*>(xs + p * xplane + boff);
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane[q]),
-                                             (lds_ptr_t)(base + AB + p * BNT * 32 + (BQ * wid + q) * 1024), 16, 0,
+                                             (lds_ptr_t)(base + AB + p * BNT * 32 + (BQ * dw + q) * 1024), 16, 0,
                                              0);
         }
     };
-    auto stage = [&](int buf, int kt) {
+    // stage sb: its KSUB 16-k steps (those before k_end)
+    auto stage = [&](int buf, int sb) {
 #pragma unroll
-        for (int d = 0; d < NDMA; ++d) stage_piece(buf, kt, d);
+        for (int u = 0; u < KSUB; ++u) {
+            const int kt = k_begin + (sb * KSUB + u) * 16;
+            if (KSUB == 1 || kt < k_end) {
+#pragma unroll
+                for (int d = 0; d < NDMA; ++d) stage_piece(buf * KSUB + u, kt, d);
+            }
+        }
     };
+
+    const int nk16 = (k_end - k_begin) >> 4;               // 16-k steps
+    const int nkt = (nk16 + KSUB - 1) / KSUB;              // stages
+    if constexpr (WS) {
+        if (loader) {
+            // stage t+3 into the slot the compute waves finished with before
+            // barrier t; before barrier t, stage t has landed (t+1, t+2 may not)
+            for (int sb = 0; sb < NS - 1 && sb < nkt; ++sb) stage(sb, sb);
+            for (int t = 0; t < nkt; ++t) {
+                const int ahead = min(NS - 2, nkt - 1 - t);
+                if (ahead >= 2) vm_wait<2 * NDMA>();
+                else if (ahead == 1) vm_wait<NDMA>();
+                else vm_wait<0>();
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                if (t + NS - 1 < nkt) stage((t + NS - 1) % NS, t + NS - 1);
+            }
+            return;
+        }
+    }
 
     // accumulators start at bias (+ residual): see conv.hip conv_fwd_kernel
     const int li = lane & 31, h = lane >> 5;
@@ -564,28 +606,32 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
     const bool direct = slab == nullptr;
     ubpl::seed_acc<TM, TN, true>(acc, direct ? bias : nullptr, direct ? res : nullptr, obase, m0 + wm, Cout, P);
 
-    const int nkt = (k_end - k_begin) >> 4;
-    if (nkt > 0) stage(0, k_begin);
-    if (NS == 3 && nkt > 1) stage(1, k_begin + 16);
+    if (!WS && nkt > 0) stage(0, 0);
+    if (!WS && NS == 3 && nkt > 1) stage(1, 1);
     for (int t = 0; t < nkt; ++t) {
         // retire stage t (this wave's DMA), then the barrier: every wave's
         // stage t has landed and every wave is done reading stage t-1
-        if (NS == 3 && t + 1 < nkt) {
-            if (a_issue) vm_wait<NP + BQ * NP>();
-            else vm_wait<BQ * NP>();
-        } else {
-            if (!UBPL_PSA_NOWAIT) vm_wait<0>();
+        if constexpr (!WS) {
+            if (NS == 3 && t + 1 < nkt && (KSUB == 1 || (t + 2) * KSUB <= nk16)) {
+                if (a_issue) vm_wait<KSUB * (NP + BQ * NP)>();
+                else vm_wait<KSUB * BQ * NP>();
+            } else {
+                if (!UBPL_PSA_NOWAIT) vm_wait<0>();
+            }
         }
         if (!UBPL_PSA_NOBAR) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         // UBPL_PSA_DMA_IL: the ping-pong body issues the next stage's DMA pieces
         // between its MFMA chains instead of all of them ahead of the first chain
-        constexpr bool IL = UBPL_PSA_DMA_IL && NP == 3 && TN > 2 && UBPL_PSA_PP;
-        const bool do_stage = t + NS - 1 < nkt;
+        constexpr bool IL = UBPL_PSA_DMA_IL && NP == 3 && TN > 2 && UBPL_PSA_PP && KSUB == 1 && !WS;
+        const bool do_stage = !WS && t + NS - 1 < nkt;
         const int sbuf = (t + NS - 1) % NS, skt = k_begin + (t + NS - 1) * 16;
-        if (!IL && do_stage) stage(sbuf, skt);
+        if (!IL && do_stage) stage(sbuf, t + NS - 1);
+#pragma unroll
+        for (int u = 0; u < KSUB; ++u) {
+        if (KSUB > 1 && (t * KSUB + u) >= nk16) break;
         const int cur = t % NS;
-        const char* base = lds + cur * (AB + BB);
+        const char* base = lds + (cur * KSUB + u) * SB;
         bf16x8 af[TM][NP], bfr[TN][NP];
         auto read_b = [&](int j) {
             const int row = wn + 32 * j + li;
@@ -680,6 +726,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 #pragma unroll
                 for (int j = 0; j < TN; ++j) mfma_split<NP>(acc[i][j], af[i], bfr[j]);
         }
+        }   // sub-steps
         // fragments consumed (the MFMAs waited on them) before the next barrier
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -1685,7 +1732,7 @@ Plan fwd_plan(int Cout, int64_t N, int Ktot, int np, bool psa = false) {
 void launch_split_reduce(const float* slab, int splits, int Cout, int P, int64_t N, const float* bias,
                          const float* res, float* y, hipStream_t st);
 
-template <int BM, int KS, int NP, int BNT, int WGM = 2>
+template <int BM, int KS, int NP, int BNT, int WGM = 2, int KSUB = 1, bool WS = false>
 int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t wplane, const float* bias,
                const float* res, float* y, int B, int Cin, int H, int W, int pad, int Cout, const Plan& pl,
                float* slab, float* stat_part, const ubpl::BnBwdEpi& bwd, hipStream_t st) {
@@ -1694,10 +1741,11 @@ int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t w
     const bool split = pl.splits > 1;
     const ubpl::BnBwdEpi off{nullptr, nullptr, 0, nullptr};
     if (!split && (stat_part || bwd.part))
-        hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM, true>), grid, dim3(NT), 0, st, xs, xplane, wp,
+        hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM, true, KSUB>), grid, dim3(NT), 0, st, xs, xplane, wp,
                            wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl.kchunk, nullptr, stat_part, bwd);
     else
-        hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM>), grid, dim3(NT), 0, st, xs, xplane, wp, wplane,
+        hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM, false, KSUB, WS>), grid,
+                           dim3(WS ? 2 * NT : NT), 0, st, xs, xplane, wp, wplane,
                            bias, split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr,
                            nullptr, off);
     UBPL_LAUNCH_CHECK();
@@ -1902,27 +1950,51 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         return launch_psa<64, 4, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                             slab, stat_part, bwd, st);
     }
+    // the one-piece (bf16) path: KSUB 16-k steps per stage and barrier (UBPL_PSA_KSUB1 in 1..4)
+    static const int ksub1 = [] {
+        const char* e = getenv("UBPL_PSA_KSUB1");
+        const int v = e ? atoi(e) : PSA_KSUB1;
+        return v >= 1 && v <= 4 ? v : PSA_KSUB1;
+    }();
+#define UBPL_PSA1(BM_, KS_, WGM_)                                                                                  \
+    do {                                                                                                           \
+        switch (ksub1) {                                                                                           \
+            case 2: return launch_psa<BM_, KS_, 1, 256, WGM_, 2>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, \
+                                                                   H, W, pad, Cout, pl, slab, stat_part, bwd, st); \
+            case 3: return launch_psa<BM_, KS_, 1, 256, WGM_, 3>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, \
+                                                                   H, W, pad, Cout, pl, slab, stat_part, bwd, st); \
+            case 4: return launch_psa<BM_, KS_, 1, 256, WGM_, 4>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, \
+                                                                   H, W, pad, Cout, pl, slab, stat_part, bwd, st); \
+            default: return launch_psa<BM_, KS_, 1, 256, WGM_, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin,\
+                                                                    H, W, pad, Cout, pl, slab, stat_part, bwd, st);\
+        }                                                                                                          \
+    } while (0)
     if (bm64w && pl.bm == 64 && pl.splits == 1 && npieces != 2 && N % 256 == 0 && (KS == 3 || npieces == 1)) {
         if (npieces == 3)
             return launch_psa<64, 3, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                                 slab, stat_part, bwd, st);
-        if (KS == 3)
-            return launch_psa<64, 3, 1, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                                slab, stat_part, bwd, st);
-        return launch_psa<64, 1, 1, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                            slab, stat_part, bwd, st);
+        if (KS == 3) UBPL_PSA1(64, 3, 1);
+        UBPL_PSA1(64, 1, 1);
     }
     if (bn256 && pl.bm == 128 && pl.splits == 1 && npieces != 2 && N % 256 == 0) {
         if (npieces == 1) {
-            if (KS == 3)
-                return launch_psa<128, 3, 1, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout,
-                                                  pl, slab, stat_part, bwd, st);
-            return launch_psa<128, 1, 1, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                              slab, stat_part, bwd, st);
+            if (KS == 3) UBPL_PSA1(128, 3, 2);
+            UBPL_PSA1(128, 1, 2);
         }
-        if (KS == 3)
+        // the warp-specialized 512-thread variant (4 compute + 4 loader waves, 4-stage
+        // ring) when UBPL_PSA_WS=1 (opt-in: 350.2 vs 351.2 img/s); the
+        // epilogue-partials launches stay on 256 threads
+        static const bool ws = [] {
+            const char* e = getenv("UBPL_PSA_WS");
+            return e ? atoi(e) != 0 : PSA_WS;
+        }();
+        if (KS == 3) {
+            if (ws && !stat_part && !bwd.part)
+                return launch_psa<128, 3, 3, 256, 2, 1, true>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W,
+                                                              pad, Cout, pl, slab, stat_part, bwd, st);
             return launch_psa<128, 3, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                               slab, stat_part, bwd, st);
+        }
         return launch_psa<128, 1, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                           slab, stat_part, bwd, st);
     }
@@ -1944,6 +2016,7 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     }
 #undef UBPL_PS_BM
 #undef UBPL_PS
+#undef UBPL_PSA1
     return (int)hipErrorInvalidValue;
 }
 
