@@ -263,7 +263,8 @@ def pck_record():
            "reference_value": rlast["pck"][-1] if rlast and rlast["epoch"] == last["epoch"] else None,
            "reference_teachers": rlast["pck"][:-1] if rlast and rlast["epoch"] == last["epoch"] else None,
            "reference_source": "tests/golden/ref_pck.json (tools/ref_pck.py: the reference's train()/validate(), "
-                               "CPU, same seeds / sampler / augmentation draws)",
+                               "CPU, same seeds / sampler / augmentation draws, the reference's crop -> "
+                               "skimage rotate -> resize pixel chain restated in oracle/augment_chain.py)",
            "note": "mean-of-teachers prediction (projects/MT_UBPL.py:387)"}
     p100 = os.path.join(ROOT, "profiles", "r02_mouse_pck_hg2_e100.json")
     if os.path.exists(p100):

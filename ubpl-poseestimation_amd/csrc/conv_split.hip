@@ -57,6 +57,14 @@ namespace {
 #ifndef UBPL_PSA_NOBAR
 #define UBPL_PSA_NOBAR 0
 #endif
+// timing-only: conv_psa_kernel with no LDS-DMA at all (the compute loop on stale LDS) /
+// with no compute (the DMA ring, its waits and barriers only)
+#ifndef UBPL_PSA_NODMA
+#define UBPL_PSA_NODMA 0
+#endif
+#ifndef UBPL_PSA_NOCOMP
+#define UBPL_PSA_NOCOMP 0
+#endif
 #ifndef UBPL_SOL_NOCHUNK
 #define UBPL_SOL_NOCHUNK 0
 #endif
@@ -559,6 +567,7 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
     };
     // stage sb: its KSUB 16-k steps (those before k_end)
     auto stage = [&](int buf, int sb) {
+        if (UBPL_PSA_NODMA) return;
 #pragma unroll
         for (int u = 0; u < KSUB; ++u) {
             const int kt = k_begin + (sb * KSUB + u) * 16;
@@ -629,6 +638,7 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
         if (!IL && do_stage) stage(sbuf, t + NS - 1);
 #pragma unroll
         for (int u = 0; u < KSUB; ++u) {
+        if (UBPL_PSA_NOCOMP) break;
         if (KSUB > 1 && (t * KSUB + u) >= nk16) break;
         const int cur = t % NS;
         const char* base = lds + (cur * KSUB + u) * SB;
