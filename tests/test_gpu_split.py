@@ -541,3 +541,68 @@ def test_stem_s2d_vs_f64(B, H):
     # K = 147 keeps the exact-f32 chain below one f32 ulp (~4e-8 relative); the
     # split path rounds once per 16-term chunk (16 chunks): a few ulps is its level
     assert esp <= max(2 * e32, 4 * 2.0 ** -24), (esp, e32)
+
+
+# the halo kernel's shapes (conv_psah_kernel: 3x3 pad 1, 128- / 64-row tiles, whole
+# rows of W = 32 / 64 / 128 per 256-pixel tile): (B, Cin, H, Cout)
+HALO_CASES = [(32, 128, 64, 128), (8, 128, 128, 128), (32, 256, 32, 256), (16, 256, 64, 256),
+              (32, 64, 128, 64), (32, 128, 32, 128)]
+
+
+@pytest.mark.parametrize("teams", ["1", "2"])
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, monkeypatch):
+    """conv_psah_kernel (input halo staged once per channel group) computes the
+    same products in the same order as conv_psa_kernel (B staged per tap):
+    forward with bias + residual and the data gradient agree bit for bit, and
+    the first / last images are within the split path's bar of float64."""
+    from ubpl_amd import kernels as Kn
+    monkeypatch.setenv("UBPL_PSA_TEAMS", teams)   # one or two 4-wave teams per workgroup (W <= 64)
+    B, Cin, H, Cout = case
+    gen = torch.Generator().manual_seed(41 + Cin + H)
+    x32 = torch.randn(B, Cin, H, H, generator=gen)
+    w32 = torch.randn(Cout, Cin, 3, 3, generator=gen) / np.sqrt(Cin * 9)
+    b32 = torch.randn(Cout, generator=gen)
+    res32 = torch.randn(B, Cout, H, H, generator=gen)
+    xs = Kn.split_activation(x32.to(DEV), 3, 1)
+    ws = Kn.conv_weight_split(w32.to(DEV), 0, 3)
+    wd = Kn.conv_weight_split(w32.to(DEV), 1, 3)
+    dys = Kn.split_activation(torch.randn(B, Cout, H, H, generator=gen).to(DEV), 3, 1) if Cin == Cout else None
+    outs = {}
+    for flag in ("0", "2"):   # 2: the halo kernel required (an error if the plan cannot take it)
+        monkeypatch.setenv("UBPL_PSA_HALO", flag)
+        y = Kn.conv2d_forward_psa(xs, ws, b32.to(DEV), res=res32.to(DEV))
+        dx = Kn.conv2d_forward_psa(dys, wd, None) if dys is not None else None
+        torch.cuda.synchronize()
+        outs[flag] = (y, dx)
+    assert torch.equal(outs["0"][0], outs["2"][0])
+    if dys is not None:
+        assert torch.equal(outs["0"][1], outs["2"][1])
+    sl = [0, B - 1]
+    yref = F.conv2d(x32[sl].double(), w32.double(), b32.double(), 1, 1) + res32[sl].double()
+    y_f32 = Kn.conv2d_forward(x32[sl].to(DEV), w32.to(DEV), b32.to(DEV), 1, res=res32[sl].to(DEV))
+    e32, esp = _rel(y_f32, yref), _rel(outs["2"][0][sl], yref)
+    print("halo %s: f32 %.2e split %.2e" % (case, e32, esp))
+    assert esp <= 2 * e32 + 1e-8, (esp, e32)
+
+
+@pytest.mark.parametrize("teams", ["1", "2"])
+@pytest.mark.parametrize("case", HALO_CASES[:2] + HALO_CASES[4:])
+def test_bf16_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, monkeypatch):
+    """The one-piece (bf16) halo kernel (one stage and barrier per channel
+    group) against conv_psa_kernel's one-piece path: bit for bit."""
+    from ubpl_amd import kernels as Kn
+    monkeypatch.setenv("UBPL_PSA_TEAMS", teams)
+    B, Cin, H, Cout = case
+    gen = torch.Generator().manual_seed(43 + Cin + H)
+    x32 = torch.randn(B, Cin, H, H, generator=gen)
+    w32 = torch.randn(Cout, Cin, 3, 3, generator=gen) / np.sqrt(Cin * 9)
+    b32 = torch.randn(Cout, generator=gen)
+    xs = Kn.split_activation(x32.to(DEV), 1, 1)
+    ws = Kn.conv_weight_split(w32.to(DEV), 0, 1)
+    outs = {}
+    for flag in ("0", "2"):
+        monkeypatch.setenv("UBPL_PSA_HALO", flag)
+        outs[flag] = Kn.conv2d_forward_psa(xs, ws, b32.to(DEV))
+        torch.cuda.synchronize()
+    assert torch.equal(outs["0"], outs["2"])

@@ -65,6 +65,10 @@ namespace {
 #ifndef UBPL_PSA_NOCOMP
 #define UBPL_PSA_NOCOMP 0
 #endif
+// timing-only: the compute loop's fragments made in registers instead of read from LDS
+#ifndef UBPL_PSA_NOREAD
+#define UBPL_PSA_NOREAD 0
+#endif
 #ifndef UBPL_SOL_NOCHUNK
 #define UBPL_SOL_NOCHUNK 0
 #endif
@@ -580,6 +584,13 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
 
     const int nk16 = (k_end - k_begin) >> 4;               // 16-k steps
     const int nkt = (nk16 + KSUB - 1) / KSUB;              // stages
+    if (UBPL_PSA_NODMA) {
+        // (the ring filled once with a run-time value, so the loads are not folded)
+        const uint32_t fill = __float_as_uint(bias ? bias[0] : 0.f) & 0x3f3f3f3fu;
+        for (int o = tid * 16; o < (int)sizeof(lds); o += (WS ? 2 * NT : NT) * 16)
+            *reinterpret_cast<uint4*>(lds + o) = make_uint4(fill, fill ^ o, fill, fill);
+        __syncthreads();
+    }
     if constexpr (WS) {
         if (loader) {
             // stage t+3 into the slot the compute waves finished with before
@@ -646,16 +657,28 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
         auto read_b = [&](int j) {
             const int row = wn + 32 * j + li;
 #pragma unroll
-            for (int p = 0; p < NP; ++p)
+            for (int p = 0; p < NP; ++p) {
+                if (UBPL_PSA_NOREAD) {
+                    const uint32_t q = 0x3f003f00u + (uint32_t)((t * 7 + row + p) & 255);
+                    bfr[j][p] = __builtin_bit_cast(bf16x8, make_uint4(q, q ^ 1, q ^ 2, q ^ 3));
+                    continue;
+                }
                 bfr[j][p] = *reinterpret_cast<const bf16x8*>(base + AB + p * BNT * 32 + row * 32 +
                                                             16 * (h ^ ((row >> 3) & 1)));
+            }
         };
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int row = wm + 32 * i + li;
 #pragma unroll
-            for (int p = 0; p < NP; ++p)
+            for (int p = 0; p < NP; ++p) {
+                if (UBPL_PSA_NOREAD) {
+                    const uint32_t q = 0x3f003f00u + (uint32_t)((t * 5 + row + p) & 255);
+                    af[i][p] = __builtin_bit_cast(bf16x8, make_uint4(q, q ^ 4, q ^ 5, q ^ 6));
+                    continue;
+                }
                 af[i][p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+            }
         }
         if constexpr (NP == 3 && TN > 2 && UBPL_PSA_PP && !UBPL_PSA_NOCHUNK) {
             // ping-pong chunks: tile q's 6-MFMA chain is issued with tile q-1's
@@ -768,6 +791,242 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (m < Cout && (!UBPL_PSA_NOSTORE || acc[i][j][r] == 1234.5f)) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+            }
+    }
+}
+
+// ------------------------------------------------------------------ 3x3, input halo staged once per channel group
+// The 3x3 stride-1 conv over PSA activations (pad 1: the PSA image's own zero
+// border is the conv padding) with the B operand staged ONCE per 16-channel
+// group instead of once per (group, tap): a workgroup's 256-pixel tile is
+// R = 256 / W whole output rows of one image, whose 3x3 receptive field is
+// PSA rows oh0 .. oh0 + R + 1 x all W + 2 columns — one contiguous
+// (R + 2) (W + 2) x 32 B run per piece, copied by LDS-DMA as it lies.  The
+// nine taps then read their B fragments from that halo image at a per-tap
+// pixel offset (kh (W + 2) + kw).  conv_psa_kernel moves 9 x 256 pixels per
+// group; this kernel (R + 2)(W + 2) (396 at W = 64: 5.8x fewer B bytes through
+// the CU's L2 -> LDS path, 2.2x fewer bytes per K step in all, the weights
+// included).  Weights: the A ring of conv_psa_kernel (3 stages, one per K step
+// = (group, tap)); halo images double-buffered per group: the next group's
+// halo is issued at the group's tap 0 and retired by tap 3 (counted vmcnt).
+// One workgroup per CU (LDS 85-139 KB); BM 128: wave tile 64 x 128 (as
+// conv_psa_kernel<128, 3, NP, 256, 2>), BM 64: 64 x 64 (4 waves along the
+// pixels, as conv_psa_kernel<64, 3, NP, 256, 1>); the same ping-pong drains.
+// Halo chunk swizzle as conv_psa_kernel's rows: pixel q's two 16-B halves
+// swapped when (q >> 3) & 1 (applied on the DMA source and on the read).
+template <int WW, int NP, int BM, int TEAMS = 1>
+__global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
+                                                        const uint16_t* __restrict__ wp, int64_t wplane,
+                                                        const float* __restrict__ bias, const float* res, float* y,
+                                                        int B, int Cin, int H, int Cout) {
+    constexpr int BNT = 256 * TEAMS, R = BNT / WW, W2 = WW + 2;
+    constexpr int NW = 4 * TEAMS;              // waves (TEAMS 4-wave teams, one 256-pixel tile each)
+    constexpr int HPX = (R + 2) * W2;          // halo pixels
+    constexpr int HI = (HPX + 31) / 32;        // DMA instructions per piece (32 pixels each)
+    constexpr int HB = HI * 1024;              // halo image bytes per piece
+    constexpr int HTOT = NP * HI;
+    constexpr int NH = (HTOT + NW - 1) / NW;   // halo DMA instructions per wave (the tail's spares: dummy slot)
+    constexpr int AB = NP * BM * 32;           // A bytes per K step
+    constexpr int AI = NP * BM / 32;           // A DMA instructions per K step (32 rows each)
+    constexpr int NAW = (AI + NW - 1) / NW;    // per wave (spares: dummy slot)
+    // GS (the one-piece path): a stage is a whole channel group — its halo and the
+    // nine taps' A images (one barrier per 9 K steps; 8 MFMAs per wave per K step
+    // left the per-step ring bound by its barriers); NS_G slots.  Otherwise A per
+    // K step in an NA-stage ring, halos double-buffered.
+    constexpr bool GS = NP == 1;
+    constexpr int NS_G = 3 * (NP * HB + 9 * AB) + 1024 <= 160 * 1024 ? 3 : 2;
+    constexpr int NA = GS ? 9 * NS_G : (TEAMS == 2 ? 2 : 3);   // A images in the ring
+    constexpr int WGM = BM / 64, WGN = 4 / WGM;
+    constexpr int TM = 2, TN = 256 / WGN / 32;
+    static_assert(BM == 64 || BM == 128, "64- or 128-row tiles");
+    constexpr int OFF_H = NA * AB, OFF_D = OFF_H + (GS ? NS_G : 2) * NP * HB;
+    static_assert(BNT % WW == 0 && WW % 32 == 0, "whole rows of 32-pixel fragments");
+    __shared__ __attribute__((aligned(16))) char lds[OFF_D + 1024];
+
+    const int P = H * WW, Hp = H + 2, G = Cin >> 4;
+    const int64_t N = (int64_t)B * P;
+    const int Ktot = Cin * 9;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = ((wid & 3) / WGN) * 64, wn = (wid >> 2) * 256 + ((wid & 3) % WGN) * (256 / WGN);
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    const int by = lam % gridDim.y, bx = lam / gridDim.y;
+    const int m0 = by * BM;
+    const int64_t n0 = (int64_t)bx * BNT;
+    const int tpi = H / R;                     // tiles per image
+    const int b = bx / tpi, oh0 = (bx - b * tpi) * R;
+
+    const int lr = lane >> 1;
+    const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
+    // A instruction i = wid * NAW + u: piece i / (BM / 32), rows 32 (i % (BM / 32)) ..
+    uint32_t a_lane[NAW];
+#pragma unroll
+    for (int u = 0; u < NAW; ++u) {
+        const int i = min(wid * NAW + u, AI - 1), rb = i % (BM / 32);
+        a_lane[u] = (uint32_t)(((int64_t)min(m0 + 32 * rb + lr, Cout - 1) * Ktot + 8 * lchunk) * 2);
+    }
+    auto stage_a = [&](int slot, int s) {
+        const char* base = reinterpret_cast<const char*>(wp + s * 16);
+#pragma unroll
+        for (int u = 0; u < NAW; ++u) {
+            const int i = wid * NAW + u;
+            const int p = i < AI ? i / (BM / 32) : 0, rb = i < AI ? i % (BM / 32) : 0;
+            char* dst = i < AI ? lds + slot * AB + p * BM * 32 + rb * 1024 : lds + OFF_D;
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(base + (int64_t)p * wplane * 2 + a_lane[u]),
+                                             (lds_ptr_t)dst, 16, 0, 0);
+        }
+    };
+    // halo of group cg: instruction i = wid * NH + u (piece i / HI, 32-pixel chunk i % HI)
+    auto stage_h = [&](int buf, int cg) {
+        const int64_t gpx = (((int64_t)b * G + cg) * Hp + oh0) * W2;   // first halo pixel (PSA pixel index)
+#pragma unroll
+        for (int u = 0; u < NH; ++u) {
+            const int i = wid * NH + u;
+            const int p = i < HTOT ? i / HI : 0, c = i < HTOT ? i - (i / HI) * HI : 0;
+            const int q = min(c * 32 + lr, HPX - 1);
+            const int ch = (lane & 1) ^ ((q >> 3) & 1);
+            const char* src = reinterpret_cast<const char*>(xs + p * xplane + (gpx + q) * 16) + ch * 16;
+            char* dst = i < HTOT ? lds + OFF_H + (buf * NP + p) * HB + c * 1024 : lds + OFF_D;
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
+        }
+    };
+
+    const int li = lane & 31, h = lane >> 5;
+    // output offsets: computed for the seed and again for the stores (not live
+    // across the K loop: register budget of the two-team variant)
+    auto out_base = [&](int64_t (&obase)[TN], bool (&nok)[TN]) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int64_t n = n0 + wn + 32 * j + li;
+            nok[j] = n < N;
+            const int64_t nc = nok[j] ? n : N - 1;
+            const int bb = (int)(nc / P);
+            const int pp = (int)(nc - (int64_t)bb * P);
+            obase[j] = (int64_t)bb * Cout * P + pp;
+        }
+    };
+    // halo pixel of tap (0, 0) for tile-local output pixel nt: row nt / WW, column nt % WW
+    const int nt0 = wn + li;
+    floatx16 acc[TM][TN];
+    {
+        int64_t obase[TN];
+        bool nok[TN];
+        out_base(obase, nok);
+        ubpl::seed_acc<TM, TN, true>(acc, bias, res, obase, m0 + wm, Cout, P);
+    }
+
+    // one K step (group cg's tap at pixel offset toff): fragments from the A image
+    // at abase and the halo image at hbase
+    auto step = [&](const char* abase, const char* hbase, int toff) {
+        bf16x8 af[TM][NP], bfr[TN][NP];
+        auto read_b = [&](int j) {
+            const int nt = nt0 + 32 * j;
+            const int q = nt + (nt / WW) * 2 + toff;
+            const char* rp = hbase + q * 32 + 16 * (h ^ ((q >> 3) & 1));
+#pragma unroll
+            for (int p = 0; p < NP; ++p) bfr[j][p] = *reinterpret_cast<const bf16x8*>(rp + p * HB);
+        };
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int row = wm + 32 * i + li;
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                af[i][p] = *reinterpret_cast<const bf16x8*>(abase + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+        }
+        if constexpr (NP == 1) {
+            // one MFMA per tile, accumulated directly (conv_psa_kernel's one-piece path)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) read_b(j);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) mfma_split<NP>(acc[i][j], af[i], bfr[j]);
+        } else {
+            // ping-pong chunks (conv_psa_kernel): tile q's chain with tile q-1's drain adds in its gaps
+#pragma unroll
+            for (int j = 0; j < TN / 2; ++j) read_b(j);
+            __builtin_amdgcn_sched_barrier(0);
+            floatx16 prev = mfma_split0<NP>(af[0], bfr[0]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = TN / 2; j < TN; ++j) read_b(j);
+#pragma unroll
+            for (int q = 1; q < TM * TN; ++q) {
+                const int j = q / TM, i = q % TM, pj = (q - 1) / TM, pi = (q - 1) % TM;
+                const floatx16 cur = mfma_split0<NP>(af[i], bfr[j]);
+                drain(acc[pi][pj], prev);
+#pragma unroll
+                for (int g = 0; g < 6; ++g) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                prev = cur;
+            }
+            drain(acc[TM - 1][TN - 1], prev);
+        }
+    };
+
+    if constexpr (GS) {
+        // one stage per channel group (halo + the nine taps' A images), NS_G-slot
+        // ring, one barrier per group
+        auto stage_g = [&](int slot, int cg) {
+            stage_h(slot, cg);
+#pragma unroll
+            for (int tp = 0; tp < 9; ++tp) stage_a(slot * 9 + tp, cg * 9 + tp);
+        };
+        for (int c = 0; c < NS_G - 1 && c < G; ++c) stage_g(c, c);
+        for (int cg = 0; cg < G; ++cg) {
+            // group cg landed; (3 slots) group cg+1 may stay in flight
+            if (NS_G == 3 && cg + 1 < G) vm_wait<NH + 9 * NAW>();
+            else vm_wait<0>();
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (cg + NS_G - 1 < G) stage_g((cg + NS_G - 1) % NS_G, cg + NS_G - 1);
+            const int slot = cg % NS_G;
+            const char* hbase = lds + OFF_H + slot * NP * HB;
+#pragma unroll 1
+            for (int tp = 0; tp < 9; ++tp) {
+                const int kh = tp / 3;
+                step(lds + (slot * 9 + tp) * AB, hbase, kh * W2 + (tp - 3 * kh));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    } else {
+        const int nk = G * 9;
+        stage_h(0, 0);
+        for (int a = 0; a < NA - 1 && a < nk; ++a) stage_a(a, a);
+        for (int s = 0; s < nk; ++s) {
+            const int cg = s / 9, tap = s - cg * 9;
+            // A(s) and (tap 0) halo(cg) landed; the A images issued after A(s) (NA - 2
+            // of them) and the next group's halo, when issued after A(s), may stay in flight
+            if (s + 1 < nk) {
+                if (tap >= 1 && tap <= NA - 1 && cg + 1 < G) vm_wait<(NA - 2) * NAW + NH>();
+                else vm_wait<(NA - 2) * NAW>();
+            } else {
+                vm_wait<0>();
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (s + NA - 1 < nk) stage_a((s + NA - 1) % NA, s + NA - 1);
+            if (tap == 0 && cg + 1 < G) stage_h((cg + 1) & 1, cg + 1);
+            const int kh = tap / 3;
+            step(lds + (s % NA) * AB, lds + OFF_H + (cg & 1) * NP * HB, kh * W2 + (tap - 3 * kh));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    }
+
+    int64_t obase[TN];
+    bool nok[TN];
+    out_base(obase, nok);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        if (!nok[j]) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < Cout) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
             }
     }
 }
@@ -1979,6 +2238,72 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
                                                                     H, W, pad, Cout, pl, slab, stat_part, bwd, st);\
         }                                                                                                          \
     } while (0)
+    // 3x3 stride-1 pad-1 on the 6xbf16 / bf16 paths, 128- or 64-row tiles, whole-row 256-pixel
+    // tiles: the input halo staged once per channel group (conv_psah_kernel);
+    // Default: the one-piece path at W <= 64 only — measured (tools/psa_bench.py,
+    // DESIGN §6): bf16 54.6 vs 59.4 us (128 ch, 64x64), 184 vs 206 (256 ch), 22.0
+    // vs 27.0 (128 ch, 32x32), but 104 vs 87 at 128x128 and, on the 6xbf16 path,
+    // 243-273 vs 224 us (128 ch, 64x64): less DMA did not make that loop faster.
+    // UBPL_PSA_HALO=1: every eligible launch, 0: none, 2: required (a 3x3 launch
+    // the kernel cannot take is an error).  Read per call: the tests compare both
+    // kernels in one process; they compute in the same order, bit for bit.
+    const char* halo_env = getenv("UBPL_PSA_HALO");
+    const int halo_mode = halo_env ? atoi(halo_env) : -1;
+    const bool halo = halo_mode < 0 ? (npieces == 1 && W <= 64) : halo_mode != 0;
+    const bool halo_ok = KS == 3 && pad == 1 && npieces != 2 && pl.splits == 1 && !stat_part && !bwd.part &&
+                         (pl.bm == 128 || bm64w) && (W == 32 || W == 64 || W == 128) && H % (256 / W) == 0;
+    if (halo_mode == 2 && KS == 3 && npieces != 2 && !halo_ok) return (int)hipErrorInvalidValue;
+    if (halo && halo_ok) {
+        // two 4-wave teams per workgroup (512 pixels: one halo, one A ring for both,
+        // two waves per SIMD) where the grid still fills the chip; UBPL_PSA_TEAMS=1 / 2
+        const char* te = getenv("UBPL_PSA_TEAMS");
+        const int mt = (Cout + pl.bm - 1) / pl.bm;
+        const bool teams2 = (te ? atoi(te) == 2 : (N / 512) * mt >= 256) && W <= 64 && H % (512 / W) == 0;
+        if (teams2) {
+            const dim3 grid2((unsigned)(N / 512), (unsigned)mt);
+#define UBPL_PSAH2(W_, BM_)                                                                                       \
+    do {                                                                                                          \
+        if (npieces == 3)                                                                                         \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 2>), grid2, dim3(2 * NT), 0, st, xs, xplane, wsplit, \
+                               wplane, bias, res, y, B, Cin, H, Cout);                                            \
+        else                                                                                                      \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 1, BM_, 2>), grid2, dim3(2 * NT), 0, st, xs, xplane, wsplit, \
+                               wplane, bias, res, y, B, Cin, H, Cout);                                            \
+    } while (0)
+            if (pl.bm == 128) {
+                if (W == 64) UBPL_PSAH2(64, 128);
+                else UBPL_PSAH2(32, 128);
+            } else {
+                if (W == 64) UBPL_PSAH2(64, 64);
+                else UBPL_PSAH2(32, 64);
+            }
+#undef UBPL_PSAH2
+            UBPL_LAUNCH_CHECK();
+            return 0;
+        }
+        const dim3 grid((unsigned)(N / 256), (unsigned)mt);
+#define UBPL_PSAH(W_, BM_)                                                                                     \
+    do {                                                                                                          \
+        if (npieces == 3)                                                                                         \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane, \
+                               bias, res, y, B, Cin, H, Cout);                                                    \
+        else                                                                                                      \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 1, BM_>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane, \
+                               bias, res, y, B, Cin, H, Cout);                                                    \
+    } while (0)
+        if (pl.bm == 128) {
+            if (W == 64) UBPL_PSAH(64, 128);
+            else if (W == 128) UBPL_PSAH(128, 128);
+            else UBPL_PSAH(32, 128);
+        } else {
+            if (W == 64) UBPL_PSAH(64, 64);
+            else if (W == 128) UBPL_PSAH(128, 64);
+            else UBPL_PSAH(32, 64);
+        }
+#undef UBPL_PSAH
+        UBPL_LAUNCH_CHECK();
+        return 0;
+    }
     if (bm64w && pl.bm == 64 && pl.splits == 1 && npieces != 2 && N % 256 == 0 && (KS == 3 || npieces == 1)) {
         if (npieces == 3)
             return launch_psa<64, 3, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
