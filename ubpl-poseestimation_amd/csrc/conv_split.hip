@@ -809,7 +809,7 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
 // included).  Weights: the A ring of conv_psa_kernel (3 stages, one per K step
 // = (group, tap)); halo images double-buffered per group: the next group's
 // halo is issued at the group's tap 0 and retired by tap 3 (counted vmcnt).
-// One workgroup per CU (LDS 85-139 KB); BM 128: wave tile 64 x 128 (as
+// One workgroup per CU (LDS 85-160 KB); BM 128: wave tile 64 x 128 (as
 // conv_psa_kernel<128, 3, NP, 256, 2>), BM 64: 64 x 64 (4 waves along the
 // pixels, as conv_psa_kernel<64, 3, NP, 256, 1>); the same ping-pong drains.
 // Halo chunk swizzle as conv_psa_kernel's rows: pixel q's two 16-B halves
@@ -823,25 +823,27 @@ __global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t
     constexpr int NW = 4 * TEAMS;              // waves (TEAMS 4-wave teams, one 256-pixel tile each)
     constexpr int HPX = (R + 2) * W2;          // halo pixels
     constexpr int HI = (HPX + 31) / 32;        // DMA instructions per piece (32 pixels each)
-    constexpr int HB = HI * 1024;              // halo image bytes per piece
+    constexpr int HB = HPX * 32;               // halo image bytes per piece (exact: the last chunk of a
+                                               // piece starts at HPX - 32, rewriting pixels it overlaps)
     constexpr int HTOT = NP * HI;
-    constexpr int NH = (HTOT + NW - 1) / NW;   // halo DMA instructions per wave (the tail's spares: dummy slot)
+    constexpr int NH = (HTOT + NW - 1) / NW;   // halo DMA instructions per wave (spares repeat the last one)
     constexpr int AB = NP * BM * 32;           // A bytes per K step
     constexpr int AI = NP * BM / 32;           // A DMA instructions per K step (32 rows each)
-    constexpr int NAW = (AI + NW - 1) / NW;    // per wave (spares: dummy slot)
+    constexpr int NAW = (AI + NW - 1) / NW;    // per wave (spares repeat the last one)
     // GS (the one-piece path): a stage is a whole channel group — its halo and the
     // nine taps' A images (one barrier per 9 K steps; 8 MFMAs per wave per K step
     // left the per-step ring bound by its barriers); NS_G slots.  Otherwise A per
     // K step in an NA-stage ring, halos double-buffered.
     constexpr bool GS = NP == 1;
-    constexpr int NS_G = 3 * (NP * HB + 9 * AB) + 1024 <= 160 * 1024 ? 3 : 2;
-    constexpr int NA = GS ? 9 * NS_G : (TEAMS == 2 ? 2 : 3);   // A images in the ring
+    constexpr int NS_G = 3 * (NP * HB + 9 * AB) <= 160 * 1024 ? 3 : 2;
+    constexpr int NA = GS ? 9 * NS_G : 3;      // A images in the ring
     constexpr int WGM = BM / 64, WGN = 4 / WGM;
     constexpr int TM = 2, TN = 256 / WGN / 32;
     static_assert(BM == 64 || BM == 128, "64- or 128-row tiles");
-    constexpr int OFF_H = NA * AB, OFF_D = OFF_H + (GS ? NS_G : 2) * NP * HB;
+    constexpr int OFF_H = NA * AB, LDS_BYTES = OFF_H + (GS ? NS_G : 2) * NP * HB;
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS");
     static_assert(BNT % WW == 0 && WW % 32 == 0, "whole rows of 32-pixel fragments");
-    __shared__ __attribute__((aligned(16))) char lds[OFF_D + 1024];
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
 
     const int P = H * WW, Hp = H + 2, G = Cin >> 4;
     const int64_t N = (int64_t)B * P;
@@ -868,9 +870,9 @@ __global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t
         const char* base = reinterpret_cast<const char*>(wp + s * 16);
 #pragma unroll
         for (int u = 0; u < NAW; ++u) {
-            const int i = wid * NAW + u;
-            const int p = i < AI ? i / (BM / 32) : 0, rb = i < AI ? i % (BM / 32) : 0;
-            char* dst = i < AI ? lds + slot * AB + p * BM * 32 + rb * 1024 : lds + OFF_D;
+            const int i = min(wid * NAW + u, AI - 1);   // (a spare repeats the last: same bytes)
+            const int p = i / (BM / 32), rb = i % (BM / 32);
+            char* dst = lds + slot * AB + p * BM * 32 + rb * 1024;
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(base + (int64_t)p * wplane * 2 + a_lane[u]),
                                              (lds_ptr_t)dst, 16, 0, 0);
         }
@@ -880,12 +882,12 @@ __global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t
         const int64_t gpx = (((int64_t)b * G + cg) * Hp + oh0) * W2;   // first halo pixel (PSA pixel index)
 #pragma unroll
         for (int u = 0; u < NH; ++u) {
-            const int i = wid * NH + u;
-            const int p = i < HTOT ? i / HI : 0, c = i < HTOT ? i - (i / HI) * HI : 0;
-            const int q = min(c * 32 + lr, HPX - 1);
+            const int i = min(wid * NH + u, HTOT - 1);  // (a spare repeats the last: same bytes)
+            const int p = i / HI, c0 = min((i - p * HI) * 32, HPX - 32);
+            const int q = c0 + lr;
             const int ch = (lane & 1) ^ ((q >> 3) & 1);
             const char* src = reinterpret_cast<const char*>(xs + p * xplane + (gpx + q) * 16) + ch * 16;
-            char* dst = i < HTOT ? lds + OFF_H + (buf * NP + p) * HB + c * 1024 : lds + OFF_D;
+            char* dst = lds + OFF_H + (buf * NP + p) * HB + c0 * 32;
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
         }
     };
