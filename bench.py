@@ -93,13 +93,15 @@ ROOF_SHAPE = (128, 128, 3, 64, 64)   # Cin, Cout, KS, H, W of the roofline kerne
 # description.  HG8 at 384^2 runs its top hourglass level on 96x96 planes.
 ROOF = {
     "mt_ubpl": ((128, 128, 3, 64, 64), 3, SPLIT6_PEAK_TFLOPS,
-                "conv_psa_kernel<128, 3, 3, 256, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; 6xbf16 "
-                "split-f32 MFMA; f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
+                "conv_psah_kernel<64, 3, 128, 1, 1> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad, input "
+                "halo staged once per channel group; 6xbf16 split-f32 MFMA; f32-equivalent FLOP/s, peak = bf16 "
+                "dense / 6)"),
     "mt_ubpl_hg2_256_bf16": ((128, 128, 3, 64, 64), 1, 2500.0,
-                             "conv_psa_kernel (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; bf16 operands, "
-                             "f32 accumulation; peak = bf16 dense MFMA)"),
+                             "conv_psah_kernel<64, 1, 128, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad, "
+                             "input halo staged once per channel group; bf16 operands, f32 accumulation; peak = "
+                             "bf16 dense MFMA)"),
     "dualpose_hg4": ((128, 128, 3, 64, 64), 3, SPLIT6_PEAK_TFLOPS,
-                     "conv_psa_kernel<128, 3, 3, 256, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
+                     "conv_psah_kernel<64, 3, 128, 1, 1> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
                      "6xbf16; f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
     "mt_ubpl_hg8_384": ((128, 128, 3, 96, 96), 3, SPLIT6_PEAK_TFLOPS,
                         "conv_psa_kernel (3x3 conv, 128->128 ch, 96x96 planes, fwd + dgrad; 6xbf16; "
@@ -114,8 +116,9 @@ class PsaLaunches:
     """Records, during one eager step, the C-ABI argument tuple of every
     ubpl_conv2d_forward_psa call whose shape is the roofline kernel's — the
     3x3 128->128 convs on the 64x64 planes (Residual conv2 forward and its
-    data gradient), which run as ONE instantiation, conv_psa_kernel<128, 3, 3,
-    256, 2> (rocprofv3 names it so), with no split-K slab — and keeps every
+    data gradient), which run as ONE instantiation, conv_psah_kernel<64, 3, 128,
+    1, 1> on the 6xbf16 path (rocprofv3 names it so; conv_psa_kernel<128, 3, 3,
+    256, 2> with UBPL_PSA_HALO=0), with no split-K slab — and keeps every
     tensor those pointers reference alive, so the launches can be replayed."""
 
     def __init__(self, Kn, lib, shape=ROOF_SHAPE):
@@ -176,8 +179,8 @@ class PsaLaunches:
 
 
 def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config="mt_ubpl", train=None):
-    """The dominant kernel: conv_psa_kernel at the config's largest 3x3 planes
-    (headline: conv_psa_kernel<128,3,3,256,2>, the 3x3 conv on the 6xbf16 split
+    """The dominant kernel: the 3x3 conv at the config's largest 3x3 planes
+    (headline: conv_psah_kernel<64,3,128,1,1>, the 3x3 conv on the 6xbf16 split
     path at the 64x64 planes, forward + data gradient; the largest single entry
     of the rocprofv3 kernel summary, profiles/r0*_summary).
     achieved = algorithmic FLOP per launch (2*B*Cout*Cin*9*H*W; f32-equivalent
@@ -206,7 +209,10 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config=
     if not consistent:
         print("bench: roofline kernel replays sum to %.2f ms > %.2f ms/step" % (per_step_ms, ms_per_step),
               file=sys.stderr)
-    pmc = pmc_traffic("psa") if config == "mt_ubpl" else None
+    halo = os.environ.get("UBPL_PSA_HALO", "") != "0"
+    pmc = pmc_traffic("psah" if halo else "psa") if config == "mt_ubpl" else None
+    if not halo:
+        desc = desc.replace("conv_psah_kernel<64, 3, 128, 1, 1>", "conv_psa_kernel<128, 3, 3, 256, 2>")
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": (pmc or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc,
@@ -221,7 +227,8 @@ def pmc_traffic(kind):
     """HBM bytes per launch of the roofline kernel, measured by rocprofv3 --pmc
     passes over this bench command (tools/gpu_pmc.sh bench ->
     tools/pmc_roofline.py -> profiles/pmc_roofline[_psa].json); None if absent."""
-    p = os.path.join(ROOT, "profiles", "pmc_roofline_psa.json" if kind == "psa" else "pmc_roofline.json")
+    p = os.path.join(ROOT, "profiles", {"psa": "pmc_roofline_psa.json", "psah": "pmc_roofline_psah.json"}.get(
+        kind, "pmc_roofline.json"))
     if not os.path.exists(p):
         return None
     with open(p) as fh:

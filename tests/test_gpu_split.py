@@ -569,15 +569,18 @@ def test_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, monkeyp
     wd = Kn.conv_weight_split(w32.to(DEV), 1, 3)
     dys = Kn.split_activation(torch.randn(B, Cout, H, H, generator=gen).to(DEV), 3, 1) if Cin == Cout else None
     outs = {}
-    for flag in ("0", "2"):   # 2: the halo kernel required (an error if the plan cannot take it)
+    # 2: the double-buffered halo kernel required, 3: the one-buffer two-workgroup
+    # variant required (an error if the plan cannot take the launch)
+    for flag in ("0", "2", "3"):
         monkeypatch.setenv("UBPL_PSA_HALO", flag)
         y = Kn.conv2d_forward_psa(xs, ws, b32.to(DEV), res=res32.to(DEV))
         dx = Kn.conv2d_forward_psa(dys, wd, None) if dys is not None else None
         torch.cuda.synchronize()
         outs[flag] = (y, dx)
-    assert torch.equal(outs["0"][0], outs["2"][0])
-    if dys is not None:
-        assert torch.equal(outs["0"][1], outs["2"][1])
+    for flag in ("2", "3"):
+        assert torch.equal(outs["0"][0], outs[flag][0]), flag
+        if dys is not None:
+            assert torch.equal(outs["0"][1], outs[flag][1]), flag
     sl = [0, B - 1]
     yref = F.conv2d(x32[sl].double(), w32.double(), b32.double(), 1, 1) + res32[sl].double()
     y_f32 = Kn.conv2d_forward(x32[sl].to(DEV), w32.to(DEV), b32.to(DEV), 1, res=res32[sl].to(DEV))

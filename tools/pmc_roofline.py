@@ -7,7 +7,7 @@ bench.py's ConvTimer.  Bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE are KiB; gfx950's FETCH_SIZE counts half the bytes of wide reads,
 so it is doubled.  Writes profiles/pmc_roofline.json for bench.py.
 
-    python tools/pmc_roofline.py gpurun_out/pmc_bench profiles/pmc_roofline.json [source-tag] [f32|psa]
+    python tools/pmc_roofline.py gpurun_out/pmc_bench profiles/pmc_roofline.json [source-tag] [f32|psa|psah]
 
 With "psa" (conv precision 6xbf16) the roofline kernel is bench.py's:
 conv_psa_kernel<128, 3, 3, 256, 2> on 512-workgroup grids (the 128 -> 128
@@ -21,9 +21,10 @@ import re
 import sys
 
 PATS = {"f32": re.compile(r"conv_fwd_kernel<(\d+), 128, 3, 1, true, false"),
-        "psa": re.compile(r"conv_psa_kernel<128, 3, 3, 256, 2(, false)?>")}
-# psa: only the 512-workgroup launches (grid size in work-items)
-GRID = {"psa": 512 * 256}
+        "psa": re.compile(r"conv_psa_kernel<128, 3, 3, 256, 2(, false)?>"),
+        "psah": re.compile(r"conv_psah_kernel<64, 3, 128, 1, 1>")}
+# psa / psah: only the 512-workgroup launches (grid size in work-items)
+GRID = {"psa": 512 * 256, "psah": 512 * 256}
 PAT = PATS["f32"]
 KIND = "f32"
 
@@ -51,9 +52,11 @@ def main():
     nf, nw = len(fetch), len(write)
     fb = 2 * 1024 * sum(fetch.values()) / max(nf, 1)
     wb = 1024 * sum(write.values()) / max(nw, 1)
-    res = {"kernel": ("conv_fwd_kernel<*,128,3,1,PRO> (all launches of the bench step)" if kind == "f32" else
-                      "conv_psa_kernel<128, 3, 3, 256, 2> on 512-workgroup grids (3x3 128->128 at 64x64, "
-                      "B=32: forward + data gradient)"),
+    res = {"kernel": {"f32": "conv_fwd_kernel<*,128,3,1,PRO> (all launches of the bench step)",
+                      "psa": "conv_psa_kernel<128, 3, 3, 256, 2> on 512-workgroup grids (3x3 128->128 at 64x64, "
+                             "B=32: forward + data gradient)",
+                      "psah": "conv_psah_kernel<64, 3, 128, 1, 1> on 512-workgroup grids (3x3 128->128 at "
+                              "64x64, B=32: forward + data gradient)"}[kind],
            "launches_fetch_pass": nf, "launches_write_pass": nw,
            "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
            "hbm_bytes_per_launch": fb + wb,

@@ -6,10 +6,11 @@ and in the back-to-back replays bench.py times with HIP events (the last
     python tools/trace_roofline.py TRACE.csv [launches_per_step 60] [reps 10]
 """
 import csv
+import os
 import json
 import sys
 
-KERNEL = "conv_psa_kernel<128, 3, 3, 256, 2"
+KERNEL = os.environ.get("ROOF_KERNEL", "conv_psah_kernel<64, 3, 128, 1, 1>")
 
 
 def main(path, n=60, reps=10):

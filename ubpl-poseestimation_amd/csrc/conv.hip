@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(NT, 4) conv_fwd_kernel(const float* __restrict
     const int P = Ho * Wo, HWin = H * W;
     const int64_t N = (int64_t)B * P;
     const int Ktot = Cin * KS * KS;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
     const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
     // XCD-aware tile order: the m tiles of one n tile, then neighbouring n
     // tiles (shared halo rows), share an L2; split-K slowest.
@@ -348,7 +348,7 @@ __global__ void __launch_bounds__(NT, 2) conv1x1_dma_kernel(const float* __restr
     __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
 
     const int64_t N = (int64_t)B * P;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
     const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN1 / 2);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                               gridDim.x * gridDim.y * gridDim.z);
@@ -533,7 +533,7 @@ __global__ void __launch_bounds__(NT) conv_wgrad_kernel(const float* __restrict_
     const int64_t Kall = (int64_t)B * P;
     const int Ntot = Cin * KS * KS;
     const int Nt = Ntot + 1;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
     const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
     const int m0 = blockIdx.y * BM;
     const int nb0 = blockIdx.x * BN;
@@ -692,7 +692,7 @@ __global__ void __launch_bounds__(NT, 4) conv_wgrad2_kernel(const float* __restr
     const int P = Ho * Wo, HWin = H * W;
     const int Kall = B * P;
     const int Ntot = Cin * KS * KS, Nt = Ntot + 1;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
     const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
     // XCD-aware tile order: the n tiles (taps) and m tiles of one k split read
     // the same dy / x rows and share an L2.

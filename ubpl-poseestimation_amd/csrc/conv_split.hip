@@ -137,6 +137,39 @@ __device__ __forceinline__ floatx16 mfma_split0(const bf16x8 (&a)[NP], const bf1
     return t;
 }
 
+
+// The scalar epilogue of a TM x TN tile of 32 x 32 MFMA blocks (rows mrow0 + ..,
+// output offsets obase[j] + m * P): when the whole tile is in range (`full`,
+// wave-uniform) the stores go out unguarded — each guarded store had been a
+// compare, an exec-mask branch and a restore.
+template <int TM, int TN>
+__device__ __forceinline__ void store_tile(const floatx16 (&acc)[TM][TN], const bool (&nok)[TN],
+                                           const int64_t (&obase)[TN], int mrow0, int M, int P, float* y,
+                                           bool full) {
+    const int h = (threadIdx.x & 63) >> 5;
+    if (full) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    y[obase[j] + (int64_t)(mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h) * P] = acc[i][j][r];
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        if (!nok[j]) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < M) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+            }
+    }
+}
+
 // ------------------------------------------------------------------ forward
 // x NCHW f32; wp: NP planes (stride wplane elements) of the grouped tap-major
 // weights [Cout][Ktot] as bf16; Cin % 16 == 0.  Epilogue / split-K slab as
@@ -157,7 +190,7 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_split_kernel(
     const int P = Ho * Wo, HWin = H * W;
     const int64_t N = (int64_t)B * P;
     const int Ktot = Cin * T;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
     const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * (BN / 2);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                               gridDim.x * gridDim.y * gridDim.z);
@@ -515,7 +548,8 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
     const int P = H * W, Hp = H + 2 * pad, Wp = W + 2 * pad, G = Cin >> 4;
     const int64_t N = (int64_t)B * P;
     const int Ktot = Cin * T;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // (wid wave-uniform in an SGPR: the DMA index math stays scalar)
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool loader = WS && wid >= 4;
     const int dw = WS ? (wid & 3) : wid;                   // the wave's share of the DMA pieces
     const int wm = (wid / WGN) * (BM / WGM), wn = (wid % WGN) * (BNT / WGN);
@@ -782,17 +816,17 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
     }
     if (EPI && stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0 + wm, Cout, n0 + wn, N, stat_part);
     if (EPI && bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, n0 + wn, N, bwd);
+    if (UBPL_PSA_NOSTORE) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        if (!nok[j]) continue;
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < Cout && (!UBPL_PSA_NOSTORE || acc[i][j][r] == 1234.5f)) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
-            }
+                for (int r = 0; r < 16; ++r)
+                    if (nok[j] && acc[i][j][r] == 1234.5f) y[obase[j]] = acc[i][j][r];
+        return;
     }
+    store_tile<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, y, m0 + BM <= Cout && n0 + BNT <= N);
 }
 
 // ------------------------------------------------------------------ 3x3, input halo staged once per channel group
@@ -814,8 +848,11 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
 // pixels, as conv_psa_kernel<64, 3, NP, 256, 1>); the same ping-pong drains.
 // Halo chunk swizzle as conv_psa_kernel's rows: pixel q's two 16-B halves
 // swapped when (q >> 3) & 1 (applied on the DMA source and on the read).
-template <int WW, int NP, int BM, int TEAMS = 1>
-__global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
+// NHB = 1 (6xbf16, one team): ONE halo buffer and two workgroups per CU (<= 80 KB
+// each): the next group's halo is loaded after every wave finished the group's last
+// tap (a second barrier then), the partner workgroup's MFMAs covering that bubble.
+template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2>
+__global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
                                                         int B, int Cin, int H, int Cout) {
@@ -836,11 +873,12 @@ __global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t
     // K step in an NA-stage ring, halos double-buffered.
     constexpr bool GS = NP == 1;
     constexpr int NS_G = 3 * (NP * HB + 9 * AB) <= 160 * 1024 ? 3 : 2;
-    constexpr int NA = GS ? 9 * NS_G : 3;      // A images in the ring
+    static_assert(NHB == 2 || (!GS && TEAMS == 1), "one halo buffer: 6xbf16, one team");
+    constexpr int NA = GS ? 9 * NS_G : (NHB == 1 && 3 * AB + NP * HB > 80 * 1024 ? 2 : 3);   // A images
     constexpr int WGM = BM / 64, WGN = 4 / WGM;
     constexpr int TM = 2, TN = 256 / WGN / 32;
     static_assert(BM == 64 || BM == 128, "64- or 128-row tiles");
-    constexpr int OFF_H = NA * AB, LDS_BYTES = OFF_H + (GS ? NS_G : 2) * NP * HB;
+    constexpr int OFF_H = NA * AB, LDS_BYTES = OFF_H + (GS ? NS_G : NHB) * NP * HB;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS");
     static_assert(BNT % WW == 0 && WW % 32 == 0, "whole rows of 32-pixel fragments");
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
@@ -848,7 +886,8 @@ __global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t
     const int P = H * WW, Hp = H + 2, G = Cin >> 4;
     const int64_t N = (int64_t)B * P;
     const int Ktot = Cin * 9;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // (wid wave-uniform in an SGPR: the DMA index math below stays scalar)
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = ((wid & 3) / WGN) * 64, wn = (wid >> 2) * 256 + ((wid & 3) % WGN) * (256 / WGN);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int by = lam % gridDim.y, bx = lam / gridDim.y;
@@ -859,33 +898,36 @@ __global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t
 
     const int lr = lane >> 1;
     const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
-    // A instruction i = wid * NAW + u: piece i / (BM / 32), rows 32 (i % (BM / 32)) ..
-    uint32_t a_lane[NAW];
-#pragma unroll
-    for (int u = 0; u < NAW; ++u) {
-        const int i = min(wid * NAW + u, AI - 1), rb = i % (BM / 32);
-        a_lane[u] = (uint32_t)(((int64_t)min(m0 + 32 * rb + lr, Cout - 1) * Ktot + 8 * lchunk) * 2);
-    }
+    // A instruction i = u * NW + wid: piece i / (BM / 32), rows 32 (i % (BM / 32)) .. —
+    // the row block depends on the wave only (NW % (BM / 32) == 0): one lane offset
+    static_assert(NW % (BM / 32) == 0, "row block per wave");
+    const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * (wid % (BM / 32)) + lr, Cout - 1) * Ktot +
+                                        8 * lchunk) * 2);
     auto stage_a = [&](int slot, int s) {
         const char* base = reinterpret_cast<const char*>(wp + s * 16);
 #pragma unroll
         for (int u = 0; u < NAW; ++u) {
-            const int i = min(wid * NAW + u, AI - 1);   // (a spare repeats the last: same bytes)
+            // (a spare repeats the last piece's instruction for the same row block: same bytes)
+            const int i = u * NW + wid < AI ? u * NW + wid : (NP - 1) * (BM / 32) + wid % (BM / 32);
             const int p = i / (BM / 32), rb = i % (BM / 32);
             char* dst = lds + slot * AB + p * BM * 32 + rb * 1024;
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(base + (int64_t)p * wplane * 2 + a_lane[u]),
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(base + (int64_t)p * wplane * 2 + a_lane),
                                              (lds_ptr_t)dst, 16, 0, 0);
         }
     };
     // halo of group cg: instruction i = wid * NH + u (piece i / HI, 32-pixel chunk i % HI)
     auto stage_h = [&](int buf, int cg) {
         const int64_t gpx = (((int64_t)b * G + cg) * Hp + oh0) * W2;   // first halo pixel (PSA pixel index)
+        // (the lane terms made opaque here: otherwise the compiler keeps all NH per-lane
+        // source offsets live across the K loop, ~20 VGPRs, and spills the tile)
+        int lr = lane >> 1, lo = lane & 1;
+        asm volatile("" : "+v"(lr), "+v"(lo));
 #pragma unroll
         for (int u = 0; u < NH; ++u) {
             const int i = min(wid * NH + u, HTOT - 1);  // (a spare repeats the last: same bytes)
             const int p = i / HI, c0 = min((i - p * HI) * 32, HPX - 32);
             const int q = c0 + lr;
-            const int ch = (lane & 1) ^ ((q >> 3) & 1);
+            const int ch = lo ^ ((q >> 3) & 1);
             const char* src = reinterpret_cast<const char*>(xs + p * xplane + (gpx + q) * 16) + ch * 16;
             char* dst = lds + OFF_H + (buf * NP + p) * HB + c0 * 32;
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
@@ -999,6 +1041,17 @@ __global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t
         for (int a = 0; a < NA - 1 && a < nk; ++a) stage_a(a, a);
         for (int s = 0; s < nk; ++s) {
             const int cg = s / 9, tap = s - cg * 9;
+            if (NHB == 1 && tap == 0 && cg > 0) {
+                // every wave done with group cg - 1: reload the one halo buffer, wait for it
+                vm_wait<(NA - 2) * NAW>();
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                stage_h(0, cg);
+                vm_wait<0>();
+            } else if (NHB == 1) {
+                if (s + 1 < nk) vm_wait<(NA - 2) * NAW>();
+                else vm_wait<0>();
+            } else
             // A(s) and (tap 0) halo(cg) landed; the A images issued after A(s) (NA - 2
             // of them) and the next group's halo, when issued after A(s), may stay in flight
             if (s + 1 < nk) {
@@ -1010,9 +1063,9 @@ __global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             if (s + NA - 1 < nk) stage_a((s + NA - 1) % NA, s + NA - 1);
-            if (tap == 0 && cg + 1 < G) stage_h((cg + 1) & 1, cg + 1);
+            if (NHB == 2 && tap == 0 && cg + 1 < G) stage_h((cg + 1) & 1, cg + 1);
             const int kh = tap / 3;
-            step(lds + (s % NA) * AB, lds + OFF_H + (cg & 1) * NP * HB, kh * W2 + (tap - 3 * kh));
+            step(lds + (s % NA) * AB, lds + OFF_H + (NHB == 2 ? (cg & 1) : 0) * NP * HB, kh * W2 + (tap - 3 * kh));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
     }
@@ -1020,17 +1073,7 @@ __global__ void __launch_bounds__(NT * TEAMS, 1) conv_psah_kernel(const uint16_t
     int64_t obase[TN];
     bool nok[TN];
     out_base(obase, nok);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        if (!nok[j]) continue;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < Cout) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
-            }
-    }
+    store_tile<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, y, m0 + BM <= Cout && n0 + BNT <= N);
 }
 
 // ------------------------------------------------------------------ 1x1, split on load
@@ -1069,7 +1112,7 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
     __shared__ __attribute__((aligned(16))) float lds_sc[PRO ? SOL_PRO_K : 4], lds_sh[PRO ? SOL_PRO_K : 4];
 
     const int64_t N = (int64_t)B * P;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
     const int wn = 64 * wid;
     if (PRO && UBPL_SOL_LDS_COEF) {
         for (int k = tid; k < K; k += NT) {
@@ -1120,17 +1163,22 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
 
     // accumulators start at bias (+ residual): see conv_psa_kernel
     const int li = lane & 31, h = lane >> 5;
+    // output offsets: computed for the seed and again for the epilogue (not live
+    // across the K loop: the tile spilled ~30 VGPRs to scratch with them)
+    auto out_base = [&](int64_t (&ob)[TN], bool (&ok)[TN]) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int64_t n = n0 + wn + 32 * j + li;
+            ok[j] = n < N;
+            const int64_t nc = ok[j] ? n : N - 1;
+            const int b = (int)(nc / P);
+            const int p = (int)(nc - (int64_t)b * P);
+            ob[j] = (int64_t)b * M * P + p;
+        }
+    };
     int64_t obase[TN];
     bool nok[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int64_t n = n0 + wn + 32 * j + li;
-        nok[j] = n < N;
-        const int64_t nc = nok[j] ? n : N - 1;
-        const int b = (int)(nc / P);
-        const int p = (int)(nc - (int64_t)b * P);
-        obase[j] = (int64_t)b * M * P + p;
-    }
+    out_base(obase, nok);
     floatx16 acc[TM][TN];
     // UBPL_SOL_TEPI (with a residual): the output tile leaves through LDS as
     // float4 rows (8 stores per lane per 32-row block instead of 32 scalar
@@ -1263,6 +1311,7 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 
+    out_base(obase, nok);
     if (EPI && stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0, M, n0 + wn, N, stat_part);
     if (EPI && bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0, M, P, n0 + wn, N, bwd);
     if (tepi) {
@@ -1305,20 +1354,24 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
         }
         return;
     }
+    if (UBPL_SOL_NOSTORE || UBPL_SOL_NT_STORE) {   // (diagnostics)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        if (!nok[j]) continue;
+        for (int j = 0; j < TN; ++j) {
+            if (!nok[j]) continue;
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < M && (!UBPL_SOL_NOSTORE || acc[i][j][r] == 1234.5f)) {
-                    if (UBPL_SOL_NT_STORE) __builtin_nontemporal_store(acc[i][j][r], y + obase[j] + (int64_t)m * P);
-                    else y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (m < M && (!UBPL_SOL_NOSTORE || acc[i][j][r] == 1234.5f)) {
+                        if (UBPL_SOL_NT_STORE) __builtin_nontemporal_store(acc[i][j][r], y + obase[j] + (int64_t)m * P);
+                        else y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+                    }
                 }
-            }
+        }
+        return;
     }
+    store_tile<TM, TN>(acc, nok, obase, m0, M, P, y, m0 + BM <= M && n0 + BNT <= N);
 }
 
 // ------------------------------------------------------------------ 3x3 weight gradient
@@ -1359,7 +1412,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
     const int Hp = H + 2, Wp = W + 2;
     const int Gci = Cin >> 4, Gco = Cout >> 4;
     const int Ntot = 9 * Cin, Nt = Ntot + 1;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
     const int wm = (wid >> 1) * (CB / 2), wn = (wid & 1) * (CB / 2);
     // tile order: n tiles (tap, ci) fastest so the 9 taps of one K split share an L2
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
@@ -1544,7 +1597,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa64_kernel(const uint16_t* __r
     const int Hp = H + 2, Wp = W + 2;
     const int Gci = Cin >> 4, Gco = Cout >> 4;
     const int Ntot = 9 * Cin, Nt = Ntot + 1;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
     const int wm = (wid >> 1) * 32, wn = (wid & 1) * 96;
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                               gridDim.x * gridDim.y * gridDim.z);
@@ -1707,7 +1760,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad1_sol_kernel(const float* __restri
     constexpr int FA = PPA / 4, FB = PPB / 4;     // float4s per loader thread
     __shared__ __attribute__((aligned(16))) char lds[2 * SB];
 
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
     const int wm = (wid >> 1) * (CM / 2), wn = (wid & 1) * (CN / 2);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                               gridDim.x * gridDim.y * gridDim.z);
@@ -2241,26 +2294,31 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         }                                                                                                          \
     } while (0)
     // 3x3 stride-1 pad-1 on the 6xbf16 / bf16 paths, 128- or 64-row tiles, whole-row 256-pixel
-    // tiles: the input halo staged once per channel group (conv_psah_kernel);
-    // Default: the one-piece path at W <= 64 only — measured (tools/psa_bench.py,
-    // DESIGN §6): bf16 54.6 vs 59.4 us (128 ch, 64x64), 184 vs 206 (256 ch), 22.0
-    // vs 27.0 (128 ch, 32x32), but 104 vs 87 at 128x128 and, on the 6xbf16 path,
-    // 243-273 vs 224 us (128 ch, 64x64): less DMA did not make that loop faster.
-    // UBPL_PSA_HALO=1: every eligible launch, 0: none, 2: required (a 3x3 launch
-    // the kernel cannot take is an error).  Read per call: the tests compare both
-    // kernels in one process; they compute in the same order, bit for bit.
+    // tiles: the input halo staged once per channel group (conv_psah_kernel).  Default
+    // (measured, tools/psa_bench.py, profiles/r04_psa_diag.txt): the 6xbf16 path on the
+    // one-halo-buffer, two-workgroups-per-CU variant (212 vs 221 us at 128 ch 64x64, 750
+    // vs 786 at 256 ch, 250 vs 295 at 64 ch 128x128, 69 vs 75 at 128 ch 32x32); the bf16
+    // path at W <= 64 (54.6 vs 59.4 us at 128 ch 64x64, 184 vs 206 at 256 ch, 22.0 vs 27.0
+    // at 128 ch 32x32; 104 vs 87 at 128x128: not there).
+    // UBPL_PSA_HALO=0: none (conv_psa_kernel); 1: every eligible launch on the
+    // double-buffered halo (two teams where the grid fills the chip); 2: as 1, required (a
+    // 3x3 launch the kernel cannot take is an error); 3: the one-buffer variant for every
+    // eligible 6xbf16 launch, required.  Read per call: the tests compare the kernels in
+    // one process; they compute in the same order, bit for bit.
     const char* halo_env = getenv("UBPL_PSA_HALO");
     const int halo_mode = halo_env ? atoi(halo_env) : -1;
-    const bool halo = halo_mode < 0 ? (npieces == 1 && W <= 64) : halo_mode != 0;
     const bool halo_ok = KS == 3 && pad == 1 && npieces != 2 && pl.splits == 1 && !stat_part && !bwd.part &&
                          (pl.bm == 128 || bm64w) && (W == 32 || W == 64 || W == 128) && H % (256 / W) == 0;
-    if (halo_mode == 2 && KS == 3 && npieces != 2 && !halo_ok) return (int)hipErrorInvalidValue;
+    if ((halo_mode == 2 || halo_mode == 3) && KS == 3 && npieces != 2 && !halo_ok) return (int)hipErrorInvalidValue;
+    const bool one_buf = npieces == 3 && (halo_mode == 3 || halo_mode < 0);
+    const bool halo = halo_mode < 0 ? ((npieces == 1 && W <= 64) || one_buf) : halo_mode != 0;
     if (halo && halo_ok) {
         // two 4-wave teams per workgroup (512 pixels: one halo, one A ring for both,
         // two waves per SIMD) where the grid still fills the chip; UBPL_PSA_TEAMS=1 / 2
         const char* te = getenv("UBPL_PSA_TEAMS");
         const int mt = (Cout + pl.bm - 1) / pl.bm;
-        const bool teams2 = (te ? atoi(te) == 2 : (N / 512) * mt >= 256) && W <= 64 && H % (512 / W) == 0;
+        const bool teams2 = !one_buf && (te ? atoi(te) == 2 : (N / 512) * mt >= 256) && W <= 64 &&
+                            H % (512 / W) == 0;
         if (teams2) {
             const dim3 grid2((unsigned)(N / 512), (unsigned)mt);
 #define UBPL_PSAH2(W_, BM_)                                                                                       \
@@ -2284,6 +2342,23 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
             return 0;
         }
         const dim3 grid((unsigned)(N / 256), (unsigned)mt);
+        if (one_buf) {   // one halo buffer, two workgroups per CU
+#define UBPL_PSAH1(W_, BM_)                                                                                   \
+    hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 1, 1>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane, \
+                       bias, res, y, B, Cin, H, Cout)
+            if (pl.bm == 128) {
+                if (W == 64) UBPL_PSAH1(64, 128);
+                else if (W == 128) UBPL_PSAH1(128, 128);
+                else UBPL_PSAH1(32, 128);
+            } else {
+                if (W == 64) UBPL_PSAH1(64, 64);
+                else if (W == 128) UBPL_PSAH1(128, 64);
+                else UBPL_PSAH1(32, 64);
+            }
+#undef UBPL_PSAH1
+            UBPL_LAUNCH_CHECK();
+            return 0;
+        }
 #define UBPL_PSAH(W_, BM_)                                                                                     \
     do {                                                                                                          \
         if (npieces == 3)                                                                                         \
