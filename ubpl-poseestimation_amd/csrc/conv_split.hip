@@ -1089,8 +1089,11 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
 // planes of [M][K] (ubpl_conv_weights_split with KS = 1), staged as in
 // conv_psa_kernel.  2-stage ring, 2 workgroups per CU.  The activation read is
 // the f32 tensor itself: no split pass, no 6-byte/element PSA image.
-template <int BM, bool PRO, bool EPI = false, int NP = 3, int NS = 2>
-__global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const float* __restrict__ x,
+// BNT: pixels per tile, 256 (wave w: pixels 64w..64w+63) or 128 (32 per wave: half the
+// LDS and accumulators, three workgroups per CU, so one workgroup's epilogue stores run
+// beside the others' K loops)
+template <int BM, bool PRO, bool EPI = false, int NP = 3, int NS = 2, int BNT = 256>
+__global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_kernel(const float* __restrict__ x,
                                                            const uint16_t* __restrict__ wp, int64_t wplane,
                                                            const float* __restrict__ bias,
                                                            const float* __restrict__ pscale,
@@ -1100,8 +1103,9 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
     // NP = 3: 6xbf16 (f32-equivalent); NP = 1: the "bf16" precision (operands
     // rounded to bf16, one MFMA per product, accumulated in f32 directly)
     // NS: stages in the LDS ring (2, or 3 with 64-row tiles: two K steps' DMA in flight)
-    constexpr int BNT = 256;
-    constexpr int TM = BM / 32, TN = 2;
+    static_assert(BNT == 256 || BNT == 128, "256- or 128-pixel tiles");
+    constexpr int TM = BM / 32, TN = BNT / 128;
+    constexpr int BQ = BNT / 64;             // B DMA instructions per wave per K step (1 KB each)
     constexpr int AB = NP * BM * 32;         // A stage bytes: [piece][BM rows][32 B]
     constexpr int BH = 8 * BNT * 4 + 128;    // one 8-row half of the B image (+ bank shift)
     constexpr int BB = 2 * BH;
@@ -1113,7 +1117,7 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
 
     const int64_t N = (int64_t)B * P;
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
-    const int wn = 64 * wid;
+    const int wn = (BNT / 4) * wid;
     if (PRO && UBPL_SOL_LDS_COEF) {
         for (int k = tid; k < K; k += NT) {
             lds_sc[k] = pscale[k];
@@ -1134,13 +1138,16 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
     const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
     const bool a_issue = BM / 32 >= NT / 64 || wid < BM / 32;   // every wave when BM >= 128
     const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, M - 1) * K + 8 * lchunk) * 2);
-    // B DMA: wave w moves k rows 4w..4w+3, lane L pixels n0 + 4L .. +3 (P % 4 == 0)
+    // B DMA: wave w moves k rows 4w..4w+3; 256-pixel tiles: one row per instruction,
+    // lane L pixels n0 + 4L .. +3; 128-pixel tiles: two rows per instruction, lanes
+    // 32-63 the second (P % 4 == 0)
     uint32_t b_lane;
     {
-        int64_t n = n0 + 4 * lane;
+        const int pl = BNT == 256 ? lane : (lane & 31);
+        int64_t n = n0 + 4 * pl;
         n = n < N ? n : N - 4;
         const int64_t b = n / P;
-        b_lane = (uint32_t)((b * K * P + (n - b * P)) * 4);
+        b_lane = (uint32_t)((b * K * P + (n - b * P) + (BNT == 256 ? 0 : (int64_t)(lane >> 5) * P)) * 4);
     }
     auto stage = [&](int buf, int kt) {
         char* base = lds + buf * (AB + BB);
@@ -1153,8 +1160,8 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
             }
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int r = 4 * wid + q;
+        for (int q = 0; q < BQ; ++q) {
+            const int r = 4 * wid + q * (4 / BQ);
             const char* bb = reinterpret_cast<const char*>(x + (int64_t)(kt + r) * P);
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
                                              (lds_ptr_t)(base + AB + (r >> 3) * BH + (r & 7) * (BNT * 4)), 16, 0, 0);
@@ -1186,7 +1193,8 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
     // the stores, instead of seeding the accumulators with 128 scalar loads per
     // lane before the K loop (128->256 + skip at 64x64 B=32: 101 -> 91 us);
     // without a residual the scalar epilogue measured faster
-    const bool tepi = UBPL_SOL_TEPI && !EPI && res != nullptr && ((((uintptr_t)y) | (uintptr_t)res) & 15) == 0;
+    const bool tepi = UBPL_SOL_TEPI && BNT == 256 && !EPI && res != nullptr &&
+                      ((((uintptr_t)y) | (uintptr_t)res) & 15) == 0;
     ubpl::seed_acc<TM, TN>(acc, bias, tepi ? nullptr : res, obase, m0, M, P);
 
     const int nkt = K >> 4;
@@ -1196,8 +1204,8 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
         // stage t landed for every wave (NS = 3: this wave's stage t+1 DMA may stay in
         // flight), every wave done with stage t-1
         if (NS == 3 && t + 1 < nkt) {
-            if (a_issue) vm_wait<NP + 4>();
-            else vm_wait<4>();
+            if (a_issue) vm_wait<NP + BQ>();
+            else vm_wait<BQ>();
         } else {
             vm_wait<0>();
         }
@@ -1312,9 +1320,11 @@ __global__ void __launch_bounds__(NT, UBPL_SOL_LB) conv1x1_sol_kernel(const floa
     }
 
     out_base(obase, nok);
-    if (EPI && stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0, M, n0 + wn, N, stat_part);
-    if (EPI && bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0, M, P, n0 + wn, N, bwd);
-    if (tepi) {
+    if constexpr (EPI) {
+        if (stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0, M, n0 + wn, N, stat_part);
+        if (bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0, M, P, n0 + wn, N, bwd);
+    }
+    if constexpr (BNT == 256) if (tepi) {
         // every wave is done with the ring (its last reads waited on above); a
         // wave-private [32 rows][64 + 4 pixels] f32 image per 32-row block
         __syncthreads();
@@ -2490,9 +2500,15 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     const bool epi = stat_part != nullptr || bn_part != nullptr;
     if (epi && (npieces == 1 || Cout % 64 != 0)) return (int)hipErrorInvalidValue;   // (epilogue partials: 6xbf16, whole tiles)
     static const bool ns3 = sol_env("UBPL_SOL_NS", 2) == 3;
+    // UBPL_SOL_BN=128: 128-pixel tiles (three workgroups per CU) on the 6xbf16 path
+    const bool bn128 = sol_env("UBPL_SOL_BN", 256) == 128 && npieces == 3 && !epi && N % 128 == 0;
+    const dim3 grid128((unsigned)(N / 128), (unsigned)((Cout + bm - 1) / bm));
 #define UBPL_SOL(BM_, PRO_)                                                                                       \
     do {                                                                                                          \
-        if (npieces == 1)                                                                                         \
+        if (bn128)                                                                                                \
+            hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 3, 2, 128>), grid128, dim3(NT), 0, st, x,    \
+                               wsplit, wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);      \
+        else if (npieces == 1)                                                                                    \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 1>), grid, dim3(NT), 0, st, x, wsplit,       \
                                wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);              \
         else if (BM_ == 64 && ns3 && !epi)                                                                        \
