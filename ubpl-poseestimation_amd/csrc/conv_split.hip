@@ -69,6 +69,15 @@ namespace {
 #ifndef UBPL_PSA_NOREAD
 #define UBPL_PSA_NOREAD 0
 #endif
+// the one-buffer halo kernel's banded refill (build-time, opt-in: measured slower, 213-257
+// vs 211-251 us)
+#ifndef UBPL_PSAH_BAND
+#define UBPL_PSAH_BAND 0
+#endif
+// timing-only: the one-buffer halo kernel without its per-group halo reload (stale halo)
+#ifndef UBPL_PSAH_NORELOAD
+#define UBPL_PSAH_NORELOAD 0
+#endif
 #ifndef UBPL_SOL_NOCHUNK
 #define UBPL_SOL_NOCHUNK 0
 #endif
@@ -874,6 +883,12 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
     constexpr bool GS = NP == 1;
     constexpr int NS_G = 3 * (NP * HB + 9 * AB) <= 160 * 1024 ? 3 : 2;
     static_assert(NHB == 2 || (!GS && TEAMS == 1), "one halo buffer: 6xbf16, one team");
+    // NHB = 1: the next group's halo rows refilled as they fall out of use (row 0
+    // after the kh = 0 taps, row 1 after kh = 1; rows 2 .. R+1 at the group boundary,
+    // only rows 2 .. R-1 waited for there) with UBPL_PSAH_BAND=1 (build-time; slower);
+    // by default the whole halo is reloaded and waited for at each group boundary
+    constexpr bool HBAND = UBPL_PSAH_BAND != 0;
+#define BAND_W(NR_) ((NP * (((NR_) * W2 + 31) / 32) + NW - 1) / NW)
     constexpr int NA = GS ? 9 * NS_G : (NHB == 1 && 3 * AB + NP * HB > 80 * 1024 ? 2 : 3);   // A images
     constexpr int WGM = BM / 64, WGN = 4 / WGM;
     constexpr int TM = 2, TN = 256 / WGN / 32;
@@ -931,6 +946,25 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             const char* src = reinterpret_cast<const char*>(xs + p * xplane + (gpx + q) * 16) + ch * 16;
             char* dst = lds + OFF_H + (buf * NP + p) * HB + c0 * 32;
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
+        }
+    };
+    // halo rows [R0, R0 + NR) of group cg into the one buffer (NHB = 1): the band's
+    // pixels only (its last chunk starts 32 pixels before the band's end), BAND_W(NR)
+    // instructions per wave
+    auto stage_band = [&](auto r0c, auto nrc, int cg) {
+        constexpr int R0 = decltype(r0c)::value, NR = decltype(nrc)::value;
+        constexpr int BPX = NR * W2, BI = (BPX + 31) / 32, BT = NP * BI, BW = (BT + NW - 1) / NW;
+        const int64_t gpx = (((int64_t)b * G + cg) * Hp + oh0) * W2;
+        int lr = lane >> 1, lo = lane & 1;
+        asm volatile("" : "+v"(lr), "+v"(lo));
+#pragma unroll
+        for (int u = 0; u < BW; ++u) {
+            const int i = min(wid * BW + u, BT - 1);
+            const int p = i / BI, c0 = R0 * W2 + min((i - p * BI) * 32, BPX - 32);
+            const int q = c0 + lr;
+            const int ch = lo ^ ((q >> 3) & 1);
+            const char* src = reinterpret_cast<const char*>(xs + p * xplane + (gpx + q) * 16) + ch * 16;
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(lds + OFF_H + p * HB + c0 * 32), 16, 0, 0);
         }
     };
 
@@ -1041,7 +1075,30 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
         for (int a = 0; a < NA - 1 && a < nk; ++a) stage_a(a, a);
         for (int s = 0; s < nk; ++s) {
             const int cg = s / 9, tap = s - cg * 9;
-            if (NHB == 1 && tap == 0 && cg > 0) {
+            if (NHB == 1 && HBAND && tap == 0 && cg > 0) {
+                // every wave done with group cg - 1: halo rows 2 .. R-1 (rows 0 and 1 came
+                // in at taps 3 and 6 of the previous group) now, waited for; rows R, R+1
+                // (first read at taps 3 and 6) behind them, left in flight
+                vm_wait<(NA - 2) * NAW>();
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                if constexpr (R > 2) {
+                    stage_band(std::integral_constant<int, 2>{}, std::integral_constant<int, R - 2>{}, cg);
+                    vm_wait<0>();
+                }
+            } else if (NHB == 1 && HBAND) {
+                // A(s) landed; younger than it and allowed in flight: the NA - 2 A images
+                // after it, and a halo band issued after it (one issued at step u follows
+                // A(u + NA - 1): younger when s - u is 1 .. NA - 1; rows R, R+1 at tap 0,
+                // row 0 at tap 3, row 1 at tap 6)
+                const bool nxt = cg + 1 < G;
+                const int d3 = tap - 3, d6 = tap - 6;
+                if (s + 1 >= nk) vm_wait<0>();
+                else if (tap >= 1 && tap <= NA - 1 && cg > 0) vm_wait<(NA - 2) * NAW + BAND_W(2)>();
+                else if (((d3 >= 1 && d3 <= NA - 1) || (d6 >= 1 && d6 <= NA - 1)) && nxt)
+                    vm_wait<(NA - 2) * NAW + BAND_W(1)>();
+                else vm_wait<(NA - 2) * NAW>();
+            } else if (NHB == 1 && tap == 0 && cg > 0 && !UBPL_PSAH_NORELOAD) {
                 // every wave done with group cg - 1: reload the one halo buffer, wait for it
                 vm_wait<(NA - 2) * NAW>();
                 __builtin_amdgcn_s_barrier();
@@ -1064,6 +1121,14 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             asm volatile("" ::: "memory");
             if (s + NA - 1 < nk) stage_a((s + NA - 1) % NA, s + NA - 1);
             if (NHB == 2 && tap == 0 && cg + 1 < G) stage_h((cg + 1) & 1, cg + 1);
+            if constexpr (NHB == 1 && HBAND) {
+                if (tap == 0 && cg > 0)
+                    stage_band(std::integral_constant<int, R>{}, std::integral_constant<int, 2>{}, cg);
+                if (tap == 3 && cg + 1 < G)
+                    stage_band(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, cg + 1);
+                if (tap == 6 && cg + 1 < G)
+                    stage_band(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, cg + 1);
+            }
             const int kh = tap / 3;
             step(lds + (s % NA) * AB, lds + OFF_H + (NHB == 2 ? (cg & 1) : 0) * NP * HB, kh * W2 + (tap - 3 * kh));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
