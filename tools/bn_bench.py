@@ -19,7 +19,7 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
-    for C, H in ((128, 128), (128, 64), (256, 64), (128, 32), (256, 16), (256, 4)):
+    for C, H in ((128, 128), (128, 64), (256, 64), (128, 32), (256, 16), (128, 16), (256, 8), (256, 4)):
         x = torch.randn(B, C, H, H, device=dev, generator=g)
         dz = torch.randn(B, C, H, H, device=dev, generator=g)
         gamma = torch.rand(C, device=dev, generator=g) + 0.5
@@ -29,12 +29,20 @@ def main():
         dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
         out = torch.empty_like(dz)
         part = Kn.bn_bwd_partials(dz, x, sc, sh, mean, 1)
+        scratch = Kn.bn_part(B, C, dev)
+        beta = torch.zeros(C, device=dev)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        m_o, i_o, s_o, h_o = (torch.empty(C, device=dev) for _ in range(4))
+        t_fwd = timeit(lambda: Kn.bn_forward_stats(x, gamma, beta, 1e-5, 0.1, rm, rv, scratch, m_o, i_o, s_o, h_o),
+                       reps)
         t_part = timeit(lambda: Kn.bn_bwd_partials(dz, x, sc, sh, mean, 1), reps)
-        t_ready = timeit(lambda: Kn.bn_backward(dz, x, gamma, mean, istd, sc, sh, 1, part, coef, dg, db, out=out), reps)
-        t_all = timeit(lambda: Kn.bn_backward(dz, x, gamma, mean, istd, sc, sh, 1, None, coef, dg, db, out=out), reps)
+        t_ready = timeit(lambda: Kn.bn_backward(dz, x, gamma, mean, istd, sc, sh, 1, scratch, coef, dg, db, out=out,
+                                                part=part), reps)
+        t_all = timeit(lambda: Kn.bn_backward(dz, x, gamma, mean, istd, sc, sh, 1, scratch, coef, dg, db, out=out),
+                       reps)
         mb = 3 * x.numel() * 4 / 1e6
-        print("C=%3d H=%3d  partials %7.1f us | finalize+apply %7.1f us | all %7.1f us (apply %.0f MB)" % (
-            C, H, t_part * 1e3, t_ready * 1e3, t_all * 1e3, mb), flush=True)
+        print("C=%3d H=%3d  fwd stats %7.1f us | bwd partials %7.1f us | finalize+apply %7.1f us | bwd all %7.1f us"
+              " (apply %.0f MB)" % (C, H, t_fwd * 1e3, t_part * 1e3, t_ready * 1e3, t_all * 1e3, mb), flush=True)
 
 
 if __name__ == "__main__":
