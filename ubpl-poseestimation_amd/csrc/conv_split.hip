@@ -151,6 +151,13 @@ __device__ __forceinline__ floatx16 mfma_split0(const bf16x8 (&a)[NP], const bf1
 // output offsets obase[j] + m * P): when the whole tile is in range (`full`,
 // wave-uniform) the stores go out unguarded — each guarded store had been a
 // compare, an exec-mask branch and a restore.
+// the unguarded epilogue's stores non-temporal (streamed past the caches: the output is
+// read next by another kernel, far more than L2 holds): 207.5 vs 212.7 us on the 128-ch
+// 64x64 halo conv, 238 vs 252 at 64 ch 128x128, 1x1 1-3 %, the step within noise
+// (profiles/r04_psa_diag.txt); UBPL_NT_EPI=0 at build time: plain stores
+#ifndef UBPL_NT_EPI
+#define UBPL_NT_EPI 1
+#endif
 template <int TM, int TN>
 __device__ __forceinline__ void store_tile(const floatx16 (&acc)[TM][TN], const bool (&nok)[TN],
                                            const int64_t (&obase)[TN], int mrow0, int M, int P, float* y,
@@ -162,8 +169,11 @@ __device__ __forceinline__ void store_tile(const floatx16 (&acc)[TM][TN], const 
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    y[obase[j] + (int64_t)(mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h) * P] = acc[i][j][r];
+                for (int r = 0; r < 16; ++r) {
+                    float* d = y + obase[j] + (int64_t)(mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h) * P;
+                    if (UBPL_NT_EPI) __builtin_nontemporal_store(acc[i][j][r], d);
+                    else *d = acc[i][j][r];
+                }
         return;
     }
 #pragma unroll
