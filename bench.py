@@ -104,7 +104,7 @@ ROOF = {
                      "conv_psah_kernel<64, 3, 128, 1, 1> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
                      "6xbf16; f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
     "mt_ubpl_hg8_384": ((128, 128, 3, 96, 96), 3, SPLIT6_PEAK_TFLOPS,
-                        "conv_psa_kernel (3x3 conv, 128->128 ch, 96x96 planes, fwd + dgrad; 6xbf16; "
+                        "conv_psah_kernel<96, 3, 128, 1, 1, 192> (3x3 conv, 128->128 ch, 96x96 planes, fwd + dgrad; 6xbf16; "
                         "f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
     "mt_ubpl_hg8_384_bf16": ((128, 128, 3, 96, 96), 1, 2500.0,
                              "conv_psa_kernel (3x3 conv, 128->128 ch, 96x96 planes, fwd + dgrad; bf16 operands, "

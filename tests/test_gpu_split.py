@@ -609,3 +609,28 @@ def test_bf16_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, mo
         outs[flag] = Kn.conv2d_forward_psa(xs, ws, b32.to(DEV))
         torch.cuda.synchronize()
     assert torch.equal(outs["0"], outs["2"])
+
+
+@pytest.mark.parametrize("case", [(16, 128, 96, 128), (8, 256, 96, 256)])
+def test_psa_halo_kernel_96_wide_planes_bit_for_bit(case, monkeypatch):
+    """The 96-wide planes (HG8 at 384x384) on the halo kernel's 192-pixel tiles
+    (one halo buffer, UBPL_PSA_HALO=3 required) against conv_psa_kernel: forward
+    with bias + residual and the data gradient, bit for bit."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, H, Cout = case
+    gen = torch.Generator().manual_seed(47 + Cin)
+    x32 = torch.randn(B, Cin, H, H, generator=gen)
+    w32 = torch.randn(Cout, Cin, 3, 3, generator=gen) / np.sqrt(Cin * 9)
+    b32 = torch.randn(Cout, generator=gen)
+    res32 = torch.randn(B, Cout, H, H, generator=gen)
+    xs = Kn.split_activation(x32.to(DEV), 3, 1)
+    ws = Kn.conv_weight_split(w32.to(DEV), 0, 3)
+    wd = Kn.conv_weight_split(w32.to(DEV), 1, 3)
+    dys = Kn.split_activation(torch.randn(B, Cout, H, H, generator=gen).to(DEV), 3, 1)
+    outs = {}
+    for flag in ("0", "3"):
+        monkeypatch.setenv("UBPL_PSA_HALO", flag)
+        outs[flag] = (Kn.conv2d_forward_psa(xs, ws, b32.to(DEV), res=res32.to(DEV)), Kn.conv2d_forward_psa(dys, wd, None))
+        torch.cuda.synchronize()
+    assert torch.equal(outs["0"][0], outs["3"][0])
+    assert torch.equal(outs["0"][1], outs["3"][1])

@@ -23,7 +23,10 @@ def main():
     peak = PEAK if npieces == 3 else 2500.0
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
-    for cin, cout, h in ((128, 128, 64), (64, 64, 128), (128, 128, 32), (256, 256, 64)):
+    shapes = ((128, 128, 64), (64, 64, 128), (128, 128, 32), (256, 256, 64))
+    if os.environ.get("PSA_BENCH_96"):
+        shapes = ((128, 128, 96), (256, 256, 96))     # the HG8 384x384 top-level planes
+    for cin, cout, h in shapes:
         x = torch.randn(B, cin, h, h, device=dev, generator=g)
         w = torch.randn(cout, cin, 3, 3, device=dev, generator=g) * 0.05
         b = torch.randn(cout, device=dev, generator=g)

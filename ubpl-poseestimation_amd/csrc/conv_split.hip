@@ -870,12 +870,15 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
 // NHB = 1 (6xbf16, one team): ONE halo buffer and two workgroups per CU (<= 80 KB
 // each): the next group's halo is loaded after every wave finished the group's last
 // tap (a second barrier then), the partner workgroup's MFMAs covering that bubble.
-template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2>
+// BNT1: pixels per team tile — 256, or 192 for the 96-wide planes (two rows; 128-row
+// tiles only: wave tile 64 x 96, three 32-pixel fragments)
+template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2, int BNT1 = 256>
 __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
                                                         int B, int Cin, int H, int Cout) {
-    constexpr int BNT = 256 * TEAMS, R = BNT / WW, W2 = WW + 2;
+    constexpr int BNT = BNT1 * TEAMS, R = BNT / WW, W2 = WW + 2;
+    static_assert(BNT1 == 256 || (BNT1 == 192 && BM == 128), "192-pixel tiles: 128 rows");
     constexpr int NW = 4 * TEAMS;              // waves (TEAMS 4-wave teams, one 256-pixel tile each)
     constexpr int HPX = (R + 2) * W2;          // halo pixels
     constexpr int HI = (HPX + 31) / 32;        // DMA instructions per piece (32 pixels each)
@@ -901,7 +904,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
 #define BAND_W(NR_) ((NP * (((NR_) * W2 + 31) / 32) + NW - 1) / NW)
     constexpr int NA = GS ? 9 * NS_G : (NHB == 1 && 3 * AB + NP * HB > 80 * 1024 ? 2 : 3);   // A images
     constexpr int WGM = BM / 64, WGN = 4 / WGM;
-    constexpr int TM = 2, TN = 256 / WGN / 32;
+    constexpr int TM = 2, TN = BNT1 / WGN / 32;
     static_assert(BM == 64 || BM == 128, "64- or 128-row tiles");
     constexpr int OFF_H = NA * AB, LDS_BYTES = OFF_H + (GS ? NS_G : NHB) * NP * HB;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS");
@@ -913,7 +916,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
     const int Ktot = Cin * 9;
     // (wid wave-uniform in an SGPR: the DMA index math below stays scalar)
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = ((wid & 3) / WGN) * 64, wn = (wid >> 2) * 256 + ((wid & 3) % WGN) * (256 / WGN);
+    const int wm = ((wid & 3) / WGN) * 64, wn = (wid >> 2) * BNT1 + ((wid & 3) % WGN) * (BNT1 / WGN);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int by = lam % gridDim.y, bx = lam / gridDim.y;
     const int m0 = by * BM;
@@ -2392,10 +2395,14 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     // one process; they compute in the same order, bit for bit.
     const char* halo_env = getenv("UBPL_PSA_HALO");
     const int halo_mode = halo_env ? atoi(halo_env) : -1;
-    const bool halo_ok = KS == 3 && pad == 1 && npieces != 2 && pl.splits == 1 && !stat_part && !bwd.part &&
-                         (pl.bm == 128 || bm64w) && (W == 32 || W == 64 || W == 128) && H % (256 / W) == 0;
-    if ((halo_mode == 2 || halo_mode == 3) && KS == 3 && npieces != 2 && !halo_ok) return (int)hipErrorInvalidValue;
     const bool one_buf = npieces == 3 && (halo_mode == 3 || halo_mode < 0);
+    // the 96-wide planes: 192-pixel tiles on 128 rows whatever the plan's row block (its
+    // cost model is conv_psa_kernel's), the one-buffer variant only
+    const bool w96 = W == 96 && npieces == 3 && Cout % 128 == 0 && H % 2 == 0 && one_buf;
+    const bool halo_ok = KS == 3 && pad == 1 && npieces != 2 && pl.splits == 1 && !stat_part && !bwd.part &&
+                         (((pl.bm == 128 || bm64w) && (W == 32 || W == 64 || W == 128) && H % (256 / W) == 0) ||
+                          w96);
+    if ((halo_mode == 2 || halo_mode == 3) && KS == 3 && npieces != 2 && !halo_ok) return (int)hipErrorInvalidValue;
     const bool halo = halo_mode < 0 ? ((npieces == 1 && W <= 64) || one_buf) : halo_mode != 0;
     if (halo && halo_ok) {
         // two 4-wave teams per workgroup (512 pixels: one halo, one A ring for both,
@@ -2423,6 +2430,12 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
                 else UBPL_PSAH2(32, 64);
             }
 #undef UBPL_PSAH2
+            UBPL_LAUNCH_CHECK();
+            return 0;
+        }
+        if (w96) {
+            hipLaunchKernelGGL((conv_psah_kernel<96, 3, 128, 1, 1, 192>), dim3((unsigned)(N / 192), (unsigned)(Cout / 128)),
+                               dim3(NT), 0, st, xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, Cout);
             UBPL_LAUNCH_CHECK();
             return 0;
         }
