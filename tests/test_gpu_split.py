@@ -590,7 +590,7 @@ def test_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, monkeyp
 
 
 @pytest.mark.parametrize("teams", ["1", "2"])
-@pytest.mark.parametrize("case", HALO_CASES[:2] + HALO_CASES[4:])
+@pytest.mark.parametrize("case", HALO_CASES[:2] + HALO_CASES[4:] + [(16, 128, 96, 128)])
 def test_bf16_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, monkeypatch):
     """The one-piece (bf16) halo kernel (one stage and barrier per channel
     group) against conv_psa_kernel's one-piece path: bit for bit."""

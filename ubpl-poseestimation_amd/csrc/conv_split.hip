@@ -2398,7 +2398,8 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     const bool one_buf = npieces == 3 && (halo_mode == 3 || halo_mode < 0);
     // the 96-wide planes: 192-pixel tiles on 128 rows whatever the plan's row block (its
     // cost model is conv_psa_kernel's), the one-buffer variant only
-    const bool w96 = W == 96 && npieces == 3 && Cout % 128 == 0 && H % 2 == 0 && one_buf;
+    const bool w96 = W == 96 && Cout % 128 == 0 && H % 2 == 0 &&
+                     ((npieces == 3 && one_buf) || (npieces == 1 && halo_mode > 0));   // (bf16: opt-in, slower)
     const bool halo_ok = KS == 3 && pad == 1 && npieces != 2 && pl.splits == 1 && !stat_part && !bwd.part &&
                          (((pl.bm == 128 || bm64w) && (W == 32 || W == 64 || W == 128) && H % (256 / W) == 0) ||
                           w96);
@@ -2434,8 +2435,13 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
             return 0;
         }
         if (w96) {
-            hipLaunchKernelGGL((conv_psah_kernel<96, 3, 128, 1, 1, 192>), dim3((unsigned)(N / 192), (unsigned)(Cout / 128)),
-                               dim3(NT), 0, st, xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, Cout);
+            const dim3 g96((unsigned)(N / 192), (unsigned)(Cout / 128));
+            if (npieces == 3)
+                hipLaunchKernelGGL((conv_psah_kernel<96, 3, 128, 1, 1, 192>), g96, dim3(NT), 0, st, xs, xplane, wsplit,
+                                   wplane, bias, res, y, B, Cin, H, Cout);
+            else
+                hipLaunchKernelGGL((conv_psah_kernel<96, 1, 128, 1, 2, 192>), g96, dim3(NT), 0, st, xs, xplane, wsplit,
+                                   wplane, bias, res, y, B, Cin, H, Cout);
             UBPL_LAUNCH_CHECK();
             return 0;
         }
