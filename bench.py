@@ -93,15 +93,15 @@ ROOF_SHAPE = (128, 128, 3, 64, 64)   # Cin, Cout, KS, H, W of the roofline kerne
 # description.  HG8 at 384^2 runs its top hourglass level on 96x96 planes.
 ROOF = {
     "mt_ubpl": ((128, 128, 3, 64, 64), 3, SPLIT6_PEAK_TFLOPS,
-                "conv_psah_kernel<64, 3, 128, 1, 1> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad, input "
+                "conv_psah_kernel<64, 3, 128, 1, 1, 256> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad, input "
                 "halo staged once per channel group; 6xbf16 split-f32 MFMA; f32-equivalent FLOP/s, peak = bf16 "
                 "dense / 6)"),
     "mt_ubpl_hg2_256_bf16": ((128, 128, 3, 64, 64), 1, 2500.0,
-                             "conv_psah_kernel<64, 1, 128, 2> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad, "
+                             "conv_psah_kernel<64, 1, 128, 2, 2, 256> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad, "
                              "input halo staged once per channel group; bf16 operands, f32 accumulation; peak = "
                              "bf16 dense MFMA)"),
     "dualpose_hg4": ((128, 128, 3, 64, 64), 3, SPLIT6_PEAK_TFLOPS,
-                     "conv_psah_kernel<64, 3, 128, 1, 1> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
+                     "conv_psah_kernel<64, 3, 128, 1, 1, 256> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
                      "6xbf16; f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
     "mt_ubpl_hg8_384": ((128, 128, 3, 96, 96), 3, SPLIT6_PEAK_TFLOPS,
                         "conv_psah_kernel<96, 3, 128, 1, 1, 192> (3x3 conv, 128->128 ch, 96x96 planes, fwd + dgrad; 6xbf16; "
@@ -212,7 +212,7 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config=
     halo = os.environ.get("UBPL_PSA_HALO", "") != "0"
     pmc = pmc_traffic("psah" if halo else "psa") if config == "mt_ubpl" else None
     if not halo:
-        desc = desc.replace("conv_psah_kernel<64, 3, 128, 1, 1>", "conv_psa_kernel<128, 3, 3, 256, 2>")
+        desc = desc.replace("conv_psah_kernel<64, 3, 128, 1, 1, 256>", "conv_psa_kernel<128, 3, 3, 256, 2>")
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": (pmc or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc,

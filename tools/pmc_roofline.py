@@ -22,7 +22,7 @@ import sys
 
 PATS = {"f32": re.compile(r"conv_fwd_kernel<(\d+), 128, 3, 1, true, false"),
         "psa": re.compile(r"conv_psa_kernel<128, 3, 3, 256, 2(, false)?>"),
-        "psah": re.compile(r"conv_psah_kernel<64, 3, 128, 1, 1>")}
+        "psah": re.compile(r"conv_psah_kernel<64, 3, 128, 1, 1(, 256)?>")}
 # psa / psah: only the 512-workgroup launches (grid size in work-items)
 GRID = {"psa": 512 * 256, "psah": 512 * 256}
 PAT = PATS["f32"]
@@ -55,7 +55,7 @@ def main():
     res = {"kernel": {"f32": "conv_fwd_kernel<*,128,3,1,PRO> (all launches of the bench step)",
                       "psa": "conv_psa_kernel<128, 3, 3, 256, 2> on 512-workgroup grids (3x3 128->128 at 64x64, "
                              "B=32: forward + data gradient)",
-                      "psah": "conv_psah_kernel<64, 3, 128, 1, 1> on 512-workgroup grids (3x3 128->128 at "
+                      "psah": "conv_psah_kernel<64, 3, 128, 1, 1, 256> on 512-workgroup grids (3x3 128->128 at "
                               "64x64, B=32: forward + data gradient)"}[kind],
            "launches_fetch_pass": nf, "launches_write_pass": nw,
            "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,

@@ -10,7 +10,7 @@ import os
 import json
 import sys
 
-KERNEL = os.environ.get("ROOF_KERNEL", "conv_psah_kernel<64, 3, 128, 1, 1")
+KERNEL = os.environ.get("ROOF_KERNEL", "conv_psah_kernel<64, 3, 128, 1, 1, 256")
 
 
 def main(path, n=60, reps=10):
