@@ -74,6 +74,10 @@ namespace {
 #ifndef UBPL_PSAH_BAND
 #define UBPL_PSAH_BAND 0
 #endif
+// the one-buffer halo kernel's deepest A ring (stages) where the LDS allows
+#ifndef UBPL_PSAH_NA_MAX
+#define UBPL_PSAH_NA_MAX 3
+#endif
 // timing-only: the one-buffer halo kernel without its per-group halo reload (stale halo)
 #ifndef UBPL_PSAH_NORELOAD
 #define UBPL_PSAH_NORELOAD 0
@@ -902,7 +906,10 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
     // by default the whole halo is reloaded and waited for at each group boundary
     constexpr bool HBAND = UBPL_PSAH_BAND != 0;
 #define BAND_W(NR_) ((NP * (((NR_) * W2 + 31) / 32) + NW - 1) / NW)
-    constexpr int NA = GS ? 9 * NS_G : (NHB == 1 && 3 * AB + NP * HB > 80 * 1024 ? 2 : 3);   // A images
+    // (one halo buffer: as many A stages, 2 .. UBPL_PSAH_NA_MAX, as fit two workgroups per CU)
+    constexpr int NA1 = UBPL_PSAH_NA_MAX * AB + NP * HB <= 80 * 1024 ? UBPL_PSAH_NA_MAX
+                        : (3 * AB + NP * HB <= 80 * 1024 ? 3 : 2);
+    constexpr int NA = GS ? 9 * NS_G : (NHB == 1 ? NA1 : 3);   // A images
     constexpr int WGM = BM / 64, WGN = 4 / WGM;
     constexpr int TM = 2, TN = BNT1 / WGN / 32;
     static_assert(BM == 64 || BM == 128, "64- or 128-row tiles");
