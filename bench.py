@@ -209,10 +209,19 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config=
     if not consistent:
         print("bench: roofline kernel replays sum to %.2f ms > %.2f ms/step" % (per_step_ms, ms_per_step),
               file=sys.stderr)
-    halo = os.environ.get("UBPL_PSA_HALO", "") != "0"
-    pmc = pmc_traffic("psah" if halo else "psa") if config == "mt_ubpl" else None
-    if not halo:
-        desc = desc.replace("conv_psah_kernel<64, 3, 128, 1, 1, 256>", "conv_psa_kernel<128, 3, 3, 256, 2>")
+    # the kernel the dispatch picks: the default (profiles/pmc_roofline_psah.json measured it), or a
+    # UBPL_PSA_HALO override (0: the per-tap conv_psa_kernel; 1: the double-buffered halo variant),
+    # for which no traffic record exists
+    halo = os.environ.get("UBPL_PSA_HALO", "")
+    pmc = pmc_traffic("psah") if config == "mt_ubpl" and halo == "" else None
+    if halo == "0":
+        import re
+        desc = re.sub(r"conv_psah_kernel<[^>]*>", "conv_psa_kernel", desc).replace(
+            ", input halo staged once per channel group", "").replace(", input halo staged once per channel "
+                                                                      "group", "")
+    elif halo:
+        import re
+        desc = re.sub(r"conv_psah_kernel<[^>]*>", "conv_psah_kernel (UBPL_PSA_HALO=%s variant)" % halo, desc)
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": (pmc or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc,
@@ -390,17 +399,20 @@ def main():
     warm = [batches[i % 2] for i in range(a.warmup)]
     timed = [batches[i % 2] for i in range(a.steps)]
 
-    # default step (one rank): one HIP stream per network, the whole step
-    # captured in a HIP graph on the last warm-up step and replayed for the
-    # timed steps (the captured launches are the eager step's, bit for bit:
-    # tests/test_gpu_train.py); UBPL_STEP_GRAPH=0: eager launches.  Under
-    # torch.distributed the step stays eager (RCCL calls inside).
+    # default step: one HIP stream per network, the whole step captured in a
+    # HIP graph on the last warm-up step and replayed for the timed steps (the
+    # captured launches are the eager step's, bit for bit, and the replayed B=32
+    # step is checked against the reference's fixtures: tests/test_gpu_train.py);
+    # under torch.distributed captured as three segments with the two RCCL
+    # collectives between their replays (train._StepGraph); UBPL_STEP_GRAPH=0:
+    # eager launches.
     T._StepGraph.WARM = max(1, a.warmup - 1)
     train(warm, models, emas, optims, args, verbose=False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    torch.cuda._sleep(1)          # window marker for tools/prof_summary.py (a ~1-cycle spin_kernel)
     t0 = time.perf_counter()
     train(timed, models, emas, optims, args, verbose=False)
     torch.cuda.synchronize()
@@ -408,6 +420,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    torch.cuda._sleep(1)          # end marker: the kernels between the two markers are the timed steps'
     # roofline kernel: its launches from one more (eager, untimed) step, replayed
     # back to back between HIP events (standalone duration; see roofline())
     args.batch = B

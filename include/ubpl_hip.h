@@ -240,6 +240,13 @@ int ubpl_split_activation(const float* x, int B, int C, int H, int W, const floa
 /* Stride-1 conv (KS 1 or 3) of PSA activations (pad >= (KS-1)/2) with split
  * weights: both operands DMA'd global -> LDS; y = conv + bias (+ res, may alias y). */
 int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int KS, int H, int W, int npieces);
+/* Test hook (host-only): the 3x3 input-halo kernel dispatch of
+ * ubpl_conv2d_forward_psa.  halo_mode -1 default, 0 off, 1 on where eligible,
+ * 2 on and required (an ineligible 3x3 launch returns hipErrorInvalidValue),
+ * 3 the one-buffer variant required; teams -1 default, 1 / 2 teams per
+ * workgroup.  The environment (UBPL_PSA_HALO = 0 / 1, UBPL_PSA_TEAMS) sets the
+ * initial values, read once. */
+int ubpl_set_psa_dispatch(int halo_mode, int teams);
 /* 3x3 weight gradient (+ bias gradient, db nullable) on the split path from PSA
  * operands with a 1-pixel border: dys = split(dy), xs = split(conv input),
  * npieces = 3; Cin % 64 == 0, Cout % 64 == 0, W % 16 == 0. */

@@ -465,3 +465,49 @@ def test_device_code_has_no_packed_fp32_instructions(tmp_path):
         bad += re.findall(r"v_pk_(?:add|mul|fma)_f32[^\n]*", txt)[:3]
     assert n_kernels > 100
     assert not bad, bad
+
+
+def test_phase_check_flags_torch_arithmetic_only():
+    """train._PhaseCheck (UBPL_STREAM_CHECK): arithmetic on floating-point
+    tensors is recorded; views, allocations, copies, integer counters and the
+    library's own ops are not.  (CPU tensors stand in for device ones here.)"""
+    from ubpl_amd import train as T
+    x = torch.randn(4, 3)
+    n = torch.zeros(2, dtype=torch.long)
+    with T._PhaseCheck(on_device=lambda t: True) as chk:
+        x.view(12).reshape(3, 4)
+        torch.stack([x, x.clone()])
+        torch.empty_like(x).zero_()
+        x[:, 0].contiguous()
+        n.add_(1)                                # BN counters: integer, allowed
+    assert chk.seen == [], chk.seen
+    with T._PhaseCheck(on_device=lambda t: True) as chk:
+        x + 1
+        torch.where(x > 0, x, x * 2)
+        x.sum()
+    assert {"add", "mul", "sum", "where"} <= set(chk.seen), chk.seen
+
+
+def test_step_generator_collectives_in_order(monkeypatch):
+    """train._drive performs the collectives a step generator yields, in order,
+    and returns its value; the gradient all-reduce of the students is never
+    overlapped with other networks' work any more (torch's RCCL gfx950 reduce
+    kernels carry packed-FP32 adds: profiles/r05_rccl_packed_fp32.txt)."""
+    from ubpl_amd import dist as D
+    from ubpl_amd import train as T
+    calls = []
+    monkeypatch.setattr(D, "allreduce_", lambda t: calls.append(("sum", t)))
+    monkeypatch.setattr(D, "allreduce_grads", lambda ms: calls.append(("grads", ms)))
+    t, ms = torch.zeros(3), ["m0", "m1"]
+
+    def gen():
+        yield ("sum", t)
+        yield ("grads", ms)
+        return "records"
+    assert T._drive(gen()) == "records"
+    assert calls == [("sum", t), ("grads", ms)]
+    with pytest.raises(ValueError):
+        T._drive(r for r in [("bogus", None)])
+    assert not hasattr(T, "_AR_OVERLAP")
+    rec = open(os.path.join(os.path.dirname(__file__), "..", "profiles", "r05_rccl_packed_fp32.txt")).read()
+    assert "runTreeUpDown<float, FuncSum<float>" in rec

@@ -145,3 +145,59 @@ def test_dp_two_ranks_real_step(tmp_path, monkeypatch):
     # the records are the global ones (each pass-2 shard reports the global records)
     flat = lambda r: np.array([v for x in r for v in (x if isinstance(x, list) else [x])], np.float64)  # noqa: E731
     np.testing.assert_allclose(flat(r0["rec"]), flat(recs[0]), rtol=1e-6)
+
+
+def _worker_graph(rank, world, port, out):
+    """Four MT_UBPL steps per rank, eager and then captured (2 eager warm-up
+    steps, the capture as graph segments around the two collectives, replays),
+    each from freshly seeded networks."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import contextlib
+        import io
+        from ubpl_amd import train as T
+        res = {}
+        for mode in ("0", "1"):
+            os.environ["UBPL_STEP_GRAPH"] = mode
+            T._StepGraph.clear()
+            models, emas, optims, loader, args = _setup(ROWS[rank])
+            with contextlib.redirect_stdout(io.StringIO()):
+                rec = T.train_mt_ubpl(loader * 4, models, emas, optims, args)
+            runner = T._StepGraph.get(T._mt_ubpl_core, models, emas, optims, args)
+            torch.cuda.synchronize()
+            res[mode] = {"rec": rec, "segments": len(runner.graph) if runner.graph else 0,
+                         "params": [m.flat_params.cpu() for m in models + emas],
+                         "stats": [m.flat_stats.cpu() for m in models + emas]}
+            T._StepGraph.clear()
+        torch.save(res, os.path.join(out, "graph_rank%d.pt" % rank))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dp_two_ranks_segmented_graph_matches_eager(tmp_path):
+    """under torch.distributed the step is captured as
+    graph segments (forward + losses | backward + merge | AdamW + EMA +
+    records) with the two collectives run eagerly between their replays.  Two
+    gloo ranks: after 4 steps every rank's networks, BN statistics and records
+    are bit-identical to its 4 eager steps, and the replicas agree."""
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_graph, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    rs = [torch.load(os.path.join(tmp_path, "graph_rank%d.pt" % r), weights_only=True) for r in range(2)]
+    for r in rs:
+        assert r["0"]["segments"] == 0 and r["1"]["segments"] == 3
+        for what in ("params", "stats"):
+            for a, b in zip(r["0"][what], r["1"][what]):
+                assert torch.equal(a, b), what
+        assert r["0"]["rec"] == r["1"]["rec"]
+    for a, b in zip(rs[0]["1"]["params"], rs[1]["1"]["params"]):
+        assert torch.equal(a, b)

@@ -99,3 +99,25 @@ def test_headline_step_on_network_streams_repeats_bit_for_bit(monkeypatch):
         bad = [i for i, (a, b) in enumerate(zip(ref, cur)) if not torch.equal(a, b)]
         assert not bad, (r, bad)
         assert rcur == rref
+
+
+@pytest.mark.parametrize("case", ["mt_ubpl", "dualpose"])
+def test_network_phases_enqueue_no_torch_arithmetic(case, monkeypatch):
+    """the invariant the fix rests on, checked — between the fork
+    of the network streams and their join (the forwards; the backwards) no
+    PyTorch arithmetic op is enqueued (train._PhaseCheck over one eager step
+    of each multi-network project; join() raises on a violation)."""
+    from ubpl_amd import train as T
+    from ubpl_amd.hourglass import StackedHourglass
+    from ubpl_amd.optim import FlatAdamW
+    monkeypatch.setenv("UBPL_MODEL_STREAMS", "1")
+    monkeypatch.setenv("UBPL_STEP_GRAPH", "0")
+    monkeypatch.setattr(T, "_STREAM_CHECK", True)
+    cfg = seeds.step_cases()[case]
+    models, emas, _ = seeds.step_models(lambda k, s, m: StackedHourglass(k, s, m), cfg, device="cuda")
+    optims = [FlatAdamW(m, lr=cfg["lr"], weight_decay=0) for m in models]
+    loader, args = seeds.step_batch(cfg, OR.kps_heatmap_torch)
+    train = T.train_dualpose_ubpl if cfg["project"] == "DualPose_UBPL" else T.train_mt_ubpl
+    with contextlib.redirect_stdout(io.StringIO()):
+        train(loader, models, emas, optims, args)
+    torch.cuda.synchronize()

@@ -24,6 +24,16 @@ def _lib_loaded():
     _lib.load()
 
 
+@pytest.fixture()
+def _lib_dispatch():
+    """The C library (ctypes) for the halo-dispatch test hook; the default
+    dispatch is restored after the test."""
+    from ubpl_amd import _lib
+    lib = _lib.lib()
+    yield lib
+    lib.ubpl_set_psa_dispatch(-1, -1)
+
+
 def _rel(a, ref):
     a = a.detach().cpu().double()
     return float((a - ref).norm() / ref.norm())
@@ -551,13 +561,14 @@ HALO_CASES = [(32, 128, 64, 128), (8, 128, 128, 128), (32, 256, 32, 256), (16, 2
 
 @pytest.mark.parametrize("teams", ["1", "2"])
 @pytest.mark.parametrize("case", HALO_CASES)
-def test_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, monkeypatch):
+def test_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, _lib_dispatch):
     """conv_psah_kernel (input halo staged once per channel group) computes the
     same products in the same order as conv_psa_kernel (B staged per tap):
     forward with bias + residual and the data gradient agree bit for bit, and
     the first / last images are within the split path's bar of float64."""
     from ubpl_amd import kernels as Kn
-    monkeypatch.setenv("UBPL_PSA_TEAMS", teams)   # one or two 4-wave teams per workgroup (W <= 64)
+    lib = _lib_dispatch
+    lib.ubpl_set_psa_dispatch(-1, int(teams))   # one or two 4-wave teams per workgroup (W <= 64)
     B, Cin, H, Cout = case
     gen = torch.Generator().manual_seed(41 + Cin + H)
     x32 = torch.randn(B, Cin, H, H, generator=gen)
@@ -572,7 +583,7 @@ def test_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, monkeyp
     # 2: the double-buffered halo kernel required, 3: the one-buffer two-workgroup
     # variant required (an error if the plan cannot take the launch)
     for flag in ("0", "2", "3"):
-        monkeypatch.setenv("UBPL_PSA_HALO", flag)
+        lib.ubpl_set_psa_dispatch(int(flag), int(teams))
         y = Kn.conv2d_forward_psa(xs, ws, b32.to(DEV), res=res32.to(DEV))
         dx = Kn.conv2d_forward_psa(dys, wd, None) if dys is not None else None
         torch.cuda.synchronize()
@@ -591,11 +602,12 @@ def test_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, monkeyp
 
 @pytest.mark.parametrize("teams", ["1", "2"])
 @pytest.mark.parametrize("case", HALO_CASES[:2] + HALO_CASES[4:] + [(16, 128, 96, 128)])
-def test_bf16_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, monkeypatch):
+def test_bf16_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, _lib_dispatch):
     """The one-piece (bf16) halo kernel (one stage and barrier per channel
     group) against conv_psa_kernel's one-piece path: bit for bit."""
     from ubpl_amd import kernels as Kn
-    monkeypatch.setenv("UBPL_PSA_TEAMS", teams)
+    lib = _lib_dispatch
+    lib.ubpl_set_psa_dispatch(-1, int(teams))
     B, Cin, H, Cout = case
     gen = torch.Generator().manual_seed(43 + Cin + H)
     x32 = torch.randn(B, Cin, H, H, generator=gen)
@@ -605,18 +617,19 @@ def test_bf16_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, mo
     ws = Kn.conv_weight_split(w32.to(DEV), 0, 1)
     outs = {}
     for flag in ("0", "2"):
-        monkeypatch.setenv("UBPL_PSA_HALO", flag)
+        lib.ubpl_set_psa_dispatch(int(flag), int(teams))
         outs[flag] = Kn.conv2d_forward_psa(xs, ws, b32.to(DEV))
         torch.cuda.synchronize()
     assert torch.equal(outs["0"], outs["2"])
 
 
 @pytest.mark.parametrize("case", [(16, 128, 96, 128), (8, 256, 96, 256)])
-def test_psa_halo_kernel_96_wide_planes_bit_for_bit(case, monkeypatch):
+def test_psa_halo_kernel_96_wide_planes_bit_for_bit(case, _lib_dispatch):
     """The 96-wide planes (HG8 at 384x384) on the halo kernel's 192-pixel tiles
     (one halo buffer, UBPL_PSA_HALO=3 required) against conv_psa_kernel: forward
     with bias + residual and the data gradient, bit for bit."""
     from ubpl_amd import kernels as Kn
+    lib = _lib_dispatch
     B, Cin, H, Cout = case
     gen = torch.Generator().manual_seed(47 + Cin)
     x32 = torch.randn(B, Cin, H, H, generator=gen)
@@ -629,7 +642,7 @@ def test_psa_halo_kernel_96_wide_planes_bit_for_bit(case, monkeypatch):
     dys = Kn.split_activation(torch.randn(B, Cout, H, H, generator=gen).to(DEV), 3, 1)
     outs = {}
     for flag in ("0", "3"):
-        monkeypatch.setenv("UBPL_PSA_HALO", flag)
+        lib.ubpl_set_psa_dispatch(int(flag), -1)
         outs[flag] = (Kn.conv2d_forward_psa(xs, ws, b32.to(DEV), res=res32.to(DEV)), Kn.conv2d_forward_psa(dys, wd, None))
         torch.cuda.synchronize()
     assert torch.equal(outs["0"][0], outs["3"][0])

@@ -161,10 +161,69 @@ STEP_CASES = [("mt_ubpl", True), ("mt_ubpl_e0", False), ("dualpose", True), ("mt
 
 @pytest.mark.parametrize("case,flat_adam", STEP_CASES)
 def test_train_step_vs_reference(case, flat_adam, monkeypatch):
+    cfg = seeds.step_cases()[case]
+    _check_step(case, cfg, *_run_ours(cfg, flat_adam, monkeypatch))
+
+
+def _run_captured(cfg, monkeypatch):
+    """The bench's exact configuration: per-network streams, the whole step
+    captured in a HIP graph and replayed.  The graph needs WARM eager steps
+    before it captures, so: snapshot every piece of state a step changes
+    (parameters, BN running statistics and counters of all four networks,
+    AdamW moments and device step counts), run the warm-up steps, restore the
+    snapshot IN PLACE (same addresses: the graph bakes them in), then run the
+    golden batch once more — captured and replayed from the seeded state.
+    The gradients are read after the replay from the flat gradient buffers
+    (AdamW does not clear them)."""
+    from ubpl_amd import train as T
+    from ubpl_amd.optim import FlatAdamW
+    monkeypatch.setenv("UBPL_MODEL_STREAMS", "1")
+    monkeypatch.setenv("UBPL_STEP_GRAPH", "1")
+    T._StepGraph.clear()
+    models, emas, _ = seeds.step_models(_factory, cfg, device="cuda")
+    optims = [FlatAdamW(m, lr=cfg["lr"], weight_decay=0) for m in models]
+    before = [[p.detach().clone() for p in m.parameters()] for m in models + emas]
+    loader, args = seeds.step_batch(cfg, OR.kps_heatmap_torch)
+    state = [t for m in models + emas for t in (m.flat_params, m.flat_stats, m._nbt)]
+    state += [t for o in optims for t in (o.exp_avg, o.exp_avg_sq, o._step_t)]
+    snap = [t.clone() for t in state]
+    import io
+    import contextlib
+    import re
+    with contextlib.redirect_stdout(io.StringIO()):
+        T.train_mt_ubpl(list(loader) * T._StepGraph.WARM, models, emas, optims, args)
+    runner = T._StepGraph.get(T._mt_ubpl_core, models, emas, optims, args)
+    assert runner.graph is None and runner.n_eager == T._StepGraph.WARM
+    torch.cuda.synchronize()
+    for t, v in zip(state, snap):
+        t.copy_(v)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rec = T.train_mt_ubpl(loader, models, emas, optims, args)
+    assert runner.graph is not None and runner.n_eager == T._StepGraph.WARM     # this step was the replay
+    torch.cuda.synchronize()
+    counts = [[int(a), int(b)] for a, b in re.findall(r"\((\s*\d+)/(\s*\d+)\)", buf.getvalue())]
+    grads, full = {}, {}
+    for mi, m in enumerate(models):
+        grads[mi] = seeds.grad_record([(n, p.grad) for n, p in m.named_parameters()])
+        full[mi] = {n: p.grad.detach().double().cpu() for n, p in m.named_parameters() if p.grad is not None}
+    T._StepGraph.clear()
+    return models + emas, before, rec, counts, args, grads, full
+
+
+def test_captured_b32_step_vs_reference(monkeypatch):
+    """the timed path itself — the B=32 headline step
+    replayed from its captured HIP graph on per-network streams — against the
+    reference's fixtures (records, printed counts, gradient records, AdamW
+    step, EMA, BN statistics), with the bars of the eager B=32 case."""
+    case = "mt_ubpl_b32"
+    cfg = seeds.step_cases()[case]
+    _check_step(case, cfg, *_run_captured(cfg, monkeypatch))
+
+
+def _check_step(case, cfg, ours, before, rec, counts, args, grads, full):
     g = np.load(os.path.join(GD, "steps.npz"))
     g64 = np.load(os.path.join(GD, "steps64.npz"))
-    cfg = seeds.step_cases()[case]
-    ours, before, rec, counts, args, grads, full = _run_ours(cfg, flat_adam, monkeypatch)
     r, r32, r64 = np.array(_flat(rec, [])), g[case + "/records"], g64[case + "/records"]
     assert _noise_floor(r, r32, r64, np.abs(r64)).all(), (r, r32, r64)
     assert np.array_equal(np.array(counts, np.int64).reshape(-1, 2), g[case + "/printed_counts"])

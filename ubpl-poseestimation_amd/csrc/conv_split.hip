@@ -17,6 +17,7 @@
 // Weights are split once per pass (ubpl_conv_weights_split, a batched
 // re-layout into NP bf16 planes); activations are split while they are staged,
 // after the fused BN+ReLU prologue.
+#include <atomic>
 #include "common.h"
 #include <cstdlib>
 using ubpl::xcd_remap;
@@ -2337,6 +2338,35 @@ UBPL_API int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int
 // y = conv(xs, w, stride 1, pad (KS-1)/2) + bias (+ res) with xs in the PSA
 // layout (border pad >= (KS-1)/2) and w from ubpl_conv_weights_split (same
 // npieces).  KS in {1, 3}; Cin % 16 == 0; res may alias y.
+namespace {
+// dispatch knobs of the 3x3 halo kernel: from the environment once (UBPL_PSA_HALO = 0 / 1,
+// UBPL_PSA_TEAMS = 1 / 2; diagnostics), overridden by ubpl_set_psa_dispatch (tests)
+struct PsaDispatch {
+    int halo, teams;
+};
+std::atomic<int> g_psa_halo{-2}, g_psa_teams{-2};
+PsaDispatch psa_dispatch() {
+    if (g_psa_halo.load(std::memory_order_relaxed) == -2) {
+        const char* h = getenv("UBPL_PSA_HALO");
+        const char* t = getenv("UBPL_PSA_TEAMS");
+        const int hv = h ? atoi(h) : -1;
+        int expect = -2;
+        g_psa_halo.compare_exchange_strong(expect, hv == 0 || hv == 1 ? hv : -1);
+        expect = -2;
+        g_psa_teams.compare_exchange_strong(expect, t ? atoi(t) : -1);
+    }
+    return {g_psa_halo.load(std::memory_order_relaxed), g_psa_teams.load(std::memory_order_relaxed)};
+}
+}  // namespace
+
+UBPL_API int ubpl_set_psa_dispatch(int halo_mode, int teams) {
+    if (halo_mode < -1 || halo_mode > 3 || teams < -1 || teams > 2) return (int)hipErrorInvalidValue;
+    psa_dispatch();                       // the environment's values are read first, then replaced
+    g_psa_halo.store(halo_mode);
+    g_psa_teams.store(teams);
+    return 0;
+}
+
 UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                                      const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
                                      const float* res, float* y, float* slab, int npieces, float* stat_part,
@@ -2395,13 +2425,13 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     // vs 786 at 256 ch, 250 vs 295 at 64 ch 128x128, 69 vs 75 at 128 ch 32x32); the bf16
     // path at W <= 64 (54.6 vs 59.4 us at 128 ch 64x64, 184 vs 206 at 256 ch, 22.0 vs 27.0
     // at 128 ch 32x32; 104 vs 87 at 128x128: not there).
-    // UBPL_PSA_HALO=0: none (conv_psa_kernel); 1: every eligible launch on the
-    // double-buffered halo (two teams where the grid fills the chip); 2: as 1, required (a
-    // 3x3 launch the kernel cannot take is an error); 3: the one-buffer variant for every
-    // eligible 6xbf16 launch, required.  Read per call: the tests compare the kernels in
-    // one process; they compute in the same order, bit for bit.
-    const char* halo_env = getenv("UBPL_PSA_HALO");
-    const int halo_mode = halo_env ? atoi(halo_env) : -1;
+    // halo dispatch (psa_dispatch(), read once): -1 default; 0: none (conv_psa_kernel); 1:
+    // every eligible launch on the double-buffered halo (two teams where the grid fills the
+    // chip); test-only through ubpl_set_psa_dispatch: 2: as 1, required (a 3x3 launch the
+    // kernel cannot take is an error); 3: the one-buffer variant for every eligible 6xbf16
+    // launch, required.  The tests compare the kernels in one process; they compute in the
+    // same order, bit for bit.
+    const int halo_mode = psa_dispatch().halo;
     const bool one_buf = npieces == 3 && (halo_mode == 3 || halo_mode < 0);
     // the 96-wide planes: 192-pixel tiles on 128 rows whatever the plan's row block (its
     // cost model is conv_psa_kernel's), the one-buffer variant only
@@ -2415,9 +2445,9 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     if (halo && halo_ok) {
         // two 4-wave teams per workgroup (512 pixels: one halo, one A ring for both,
         // two waves per SIMD) where the grid still fills the chip; UBPL_PSA_TEAMS=1 / 2
-        const char* te = getenv("UBPL_PSA_TEAMS");
+        const int te = psa_dispatch().teams;
         const int mt = (Cout + pl.bm - 1) / pl.bm;
-        const bool teams2 = !one_buf && (te ? atoi(te) == 2 : (N / 512) * mt >= 256) && W <= 64 &&
+        const bool teams2 = !one_buf && (te > 0 ? te == 2 : (N / 512) * mt >= 256) && W <= 64 &&
                             H % (512 / W) == 0;
         if (teams2) {
             const dim3 grid2((unsigned)(N / 512), (unsigned)mt);

@@ -425,6 +425,9 @@ class StackedHourglass(nn.Module):
         if save:
             self._grad_keep = []     # the last step's upstream gradients (its streams joined since)
         ex = _Exec(self, B, dev, part, train=self.training, save=save)
+        if _RELAYOUT_ONCE and save:
+            raise RuntimeError("UBPL_RELAYOUT_ONCE is a forwards-only diagnostic: a training forward's weights "
+                               "change every step, the once-laid-out copies would go stale")
         if not (_RELAYOUT_ONCE and getattr(self, "_relaid", False)):
             self.relayout_weights(0)
             self.relayout_weights(1)       # k-major 1x1 weights for conv1x1_forward_kmajor

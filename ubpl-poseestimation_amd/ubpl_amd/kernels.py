@@ -678,7 +678,16 @@ def augment_chain(imgs, geo, cs, noise, img_mean, chan_mean, Hm, Wm, out):
             (g[:, 0] < 0).any() or (g[:, 0] >= imgs.shape[0]).any():
         raise ValueError("augment_chain: a view's stripped crop exceeds %dx%d or its source index is out of range"
                          % (Hm, Wm))
-    inter = torch.empty((V, 3, Hm, Wm), device=out.device, dtype=F32)
+    # skimage.transform.resize anti-aliases a downscale with a Gaussian of sigma = (s - 1) / 2
+    # (s = crop / output); the device resize omits it, which is exact to f32 only while its
+    # off-centre weight exp(-1 / (2 sigma^2)) stays below f32 rounding: s <= 1.3 (2e-10 there;
+    # the loaders' defaults draw s <= 1.25).  A larger crop would silently leave the reference.
+    s = max(float((g[:, 6].double() / Ho).max()), float((g[:, 7].double() / Wo).max()))
+    if s > 1.3:
+        raise ValueError("augment_chain: a crop %.3fx the output size needs skimage's anti-aliasing blur "
+                         "(sigma %.3f px), which the device resize does not run; crops up to 1.3x are exact"
+                         % (s, (s - 1) / 2))
+    inter =torch.empty((V, 3, Hm, Wm), device=out.device, dtype=F32)
     call("ubpl_augment_chain", _p(imgs), imgs.shape[1], imgs.shape[2], _p(geo), _p(cs), _p(noise), _p(img_mean),
          _p(chan_mean), V, int(Hm), int(Wm), _p(inter), Ho, Wo, _p(out))
     return out

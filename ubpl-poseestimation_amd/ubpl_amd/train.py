@@ -197,6 +197,63 @@ _SPLIT_BWD = os.environ.get("UBPL_SPLIT_BWD", "1") != "0"
 _TEACHER_STREAMS = os.environ.get("UBPL_TEACHER_STREAMS", "1") != "0"
 
 
+# Invariant of the networks' phases (fork -> join): no PyTorch arithmetic kernel
+# is enqueued — PyTorch's elementwise kernels carry packed-FP32 instructions,
+# which this hardware mis-executed beside concurrent matrix work (DESIGN.md §6;
+# the library itself is built without them, csrc/Makefile NOPK).  With
+# UBPL_STREAM_CHECK=1 every phase runs under _PhaseCheck, which records each
+# aten op on a floating-point device tensor that is not a view, an allocation
+# or a copy, and join() raises naming them (tests/test_gpu_race.py runs the
+# step so).
+_STREAM_CHECK = os.environ.get("UBPL_STREAM_CHECK") == "1"
+# data movement and metadata: no arithmetic
+_PHASE_OK = {"empty", "empty_strided", "empty_like", "zeros", "zeros_like", "zero_", "fill_", "copy_", "clone",
+             "_to_copy", "to", "cat", "stack", "detach", "alias", "view", "_unsafe_view", "reshape", "as_strided",
+             "expand", "select", "slice", "unsqueeze", "squeeze", "permute", "t", "transpose", "unbind", "split",
+             "contiguous", "record_stream", "set_", "resize_", "lift_fresh", "new_empty", "new_zeros",
+             "new_empty_strided", "split_with_sizes", "narrow", "view_as", "_reshape_alias", "unfold", "flatten",
+             "is_same_size"}
+
+
+def _phase_violation(func, args, kwargs, on_device):
+    """The aten op's name if it is arithmetic on a floating-point device tensor."""
+    if func.namespace != "aten":
+        return None
+    name = func.__name__.split(".")[0]
+    if name in _PHASE_OK:
+        return None
+    ts = [a for a in list(args) + list((kwargs or {}).values()) if torch.is_tensor(a)]
+    ts += [x for a in args if isinstance(a, (list, tuple)) for x in a if torch.is_tensor(x)]
+    if any(on_device(t) and t.is_floating_point() for t in ts):
+        return name
+    return None
+
+
+class _PhaseCheck:
+    """Records the aten arithmetic ops enqueued while the networks' streams are
+    forked (see _STREAM_CHECK).  on_device: which tensors count (the tests use
+    CPU tensors to check the classifier itself)."""
+
+    def __init__(self, on_device=lambda t: t.is_cuda):
+        from torch.utils._python_dispatch import TorchDispatchMode
+        seen = self.seen = []
+
+        class Mode(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                v = _phase_violation(func, args, kwargs, on_device)
+                if v is not None:
+                    seen.append(v)
+                return func(*args, **(kwargs or {}))
+        self.mode = Mode()
+
+    def __enter__(self):
+        self.mode.__enter__()
+        return self
+
+    def __exit__(self, *a):
+        return self.mode.__exit__(*a)
+
+
 class _ModelStreams:
     """One HIP stream per network (students 0..M-1, then their teachers).  The
     networks are independent until the losses, and their small hourglass
@@ -214,8 +271,8 @@ class _ModelStreams:
             self._cache[key] = [torch.cuda.Stream(device=dev) for _ in range(2 * M)]
         self.side = self._cache[key]
         self.M = M
-        for s in self.side:
-            s.wait_stream(self.main)
+        self._check = None
+        self.fork()
 
     @staticmethod
     def make(M, dev):
@@ -236,7 +293,22 @@ class _ModelStreams:
         """side stream of network i (students 0..M-1, their teachers M..2M-1)"""
         return self.side[0 if self._one else i]
 
+    def fork(self):
+        """Every network stream waits for main: the start of a networks' phase
+        (in a segment captured on its own it also brings the streams into the
+        capture)."""
+        for s in self.side:
+            s.wait_stream(self.main)
+        if _STREAM_CHECK and self._check is None:
+            self._check = _PhaseCheck().__enter__()
+
     def join(self, tensors=()):
+        if self._check is not None:
+            chk, self._check = self._check, None
+            chk.__exit__(None, None, None)
+            if chk.seen:
+                raise RuntimeError("ubpl_amd: PyTorch arithmetic enqueued while the network streams run "
+                                   "(UBPL_STREAM_CHECK): %s" % sorted(set(chk.seen)))
         for s in self.side:
             self.main.wait_stream(s)
         if torch.cuda.is_current_stream_capturing():
@@ -246,35 +318,57 @@ class _ModelStreams:
                 t.record_stream(self.main)
 
 
-# Under torch.distributed with per-network streams, each student's gradient
-# all-reduce is enqueued on that student's stream as soon as its backward (both
-# views: its own stream and, for the second view, its teacher's) is enqueued,
-# so RCCL moves student i's gradients while the other networks' backward still
-# runs; UBPL_AR_OVERLAP=0 all-reduces after the join (the round-2 order).
-_AR_OVERLAP = os.environ.get("UBPL_AR_OVERLAP", "1") != "0"
-
-
-def _join_and_allreduce(mstreams, models):
-    """Join the network streams, merge every student's second-view gradients,
-    SUM-all-reduce the students' gradients (projects/MT_UBPL.py:334-336 ->
-    DDP).  Same sums either way: merge, then one all-reduce per student."""
-    if mstreams is not None and _AR_OVERLAP and D.is_dist():
-        M = len(models)
-        for mi, m in enumerate(models):
-            s = mstreams.stream(mi)
-            s.wait_stream(mstreams.stream(M + mi))     # the second-view backward's stream
-            with torch.cuda.stream(s):
-                m.merge_alt_grads(release=False)
-                D.allreduce_grads([m])
-        mstreams.join()
-        for m in models:
-            m.release_backward_refs()
-        return
+# The students' gradient all-reduce runs after the network streams have joined,
+# with nothing else on the device beside it.  torch's RCCL gfx950 reduce kernels
+# carry packed-FP32 adds (runTreeUpDown<float, FuncSum>, ReduceScatter PAT f32:
+# tools/rccl_pk_check.py, profiles/r05_rccl_packed_fp32.txt), the instruction this
+# hardware mis-executed beside concurrent matrix work, so round 3's
+# overlap of student i's all-reduce with the other networks' backward (worth < 1 %
+# of the step) is gone.
+def _join_merge(mstreams, models):
+    """Join the network streams and merge every student's second-view gradients
+    (projects/MT_UBPL.py:334-336 accumulate both views into .grad)."""
     if mstreams:
         mstreams.join()
     for m in models:
         m.merge_alt_grads()
+
+
+def _join_and_allreduce(mstreams, models):
+    """_join_merge, then the SUM all-reduce of the students' gradients (-> DDP)."""
+    _join_merge(mstreams, models)
     D.allreduce_grads(models)
+
+
+# ---------------------------------------------------------------------------
+# collectives of a step generator
+# ---------------------------------------------------------------------------
+# The MT_UBPL step (_mt_ubpl_core) is a generator: it YIELDS its two exchanges —
+# ("sum", t): SUM all-reduce of the packed loss sums and counts in place (dist.py
+# exchange 1), ("grads", models): the students' gradient all-reduce (exchange 2)
+# — and whoever drives it performs them.  Eagerly they run at once (_drive); the
+# captured step under torch.distributed captures the device work between them as
+# graph segments and runs the collectives between the segments' replays
+# (_StepGraph), so the exchanges are never inside a captured graph.
+def _collective(req):
+    kind, obj = req
+    if kind == "sum":
+        D.allreduce_(obj)
+    elif kind == "grads":
+        D.allreduce_grads(obj)
+    else:
+        raise ValueError("unknown collective %r" % (kind,))
+
+
+def _drive(gen):
+    """Run a step generator eagerly: each yielded collective is performed at once."""
+    try:
+        req = gen.send(None)
+        while True:
+            _collective(req)
+            req = gen.send(None)
+    except StopIteration as e:
+        return e.value
 
 
 # AdamW + the EMA teacher update in one pass per model (FlatAdamW.step_and_ema);
@@ -319,7 +413,7 @@ class _OnMain(torch.autograd.Function):
         return g
 
 
-def _backward_all(totals, outputs=None):
+def _backward_all(totals, outputs=None, mstreams=None):
     """The reference runs total_i.backward(retain_graph=True) once per student
     (projects/MT_UBPL.py:334-336): the shared FDL term makes every call reach
     every student, so each network's backward would run M times with gradients
@@ -340,6 +434,8 @@ def _backward_all(totals, outputs=None):
     outs = [t for t in outputs if t is not None and t.requires_grad]
     grads = torch.autograd.grad(totals, outs, allow_unused=True)
     pairs = [(t, g) for t, g in zip(outs, grads) if g is not None]
+    if mstreams is not None:
+        mstreams.fork()                   # the networks' phase (a captured segment's streams join here)
     torch.autograd.backward([t for t, _ in pairs], [g for _, g in pairs])
 
 
@@ -413,8 +509,11 @@ class _StepGraph:
     into the graph's static inputs first.  Everything the step reads from the
     host — args, learning rates — is part of the cache key, so a change
     re-captures; per-step state (AdamW step counts, BN counters) lives on the
-    device.  One rank only (a collective inside the capture is not assumed
-    safe); UBPL_STEP_GRAPH=0 disables."""
+    device.  Under torch.distributed the step is captured as segments — the
+    device work before, between and after its two collectives, in one memory
+    pool, replayed in capture order — and the collectives run eagerly between
+    the replays (no collective inside a graph; gloo's host-staged all-reduce
+    and RCCL alike).  UBPL_STEP_GRAPH=0 disables."""
     WARM = 2
     _cache = {}
 
@@ -426,10 +525,11 @@ class _StepGraph:
         # §6); UBPL_STEP_GRAPH=0 disables it.
         env = os.environ.get("UBPL_STEP_GRAPH")
         want = env != "0"
-        self.enabled = want and not D.is_dist() and all(hasattr(o, "_step_t") for o in optims)
+        self.enabled = want and all(hasattr(o, "_step_t") for o in optims)
         self.hkey = None
         self.n_eager = 0
-        self.graph = None
+        self.graphs = None                 # the captured segments (one without torch.distributed)
+        self.reqs = []                     # the collective after each segment but the last
         self.key = None
         self.static = None
         self.out = None
@@ -481,13 +581,51 @@ class _StepGraph:
     def release(self):
         """Drop the captured graph, its static inputs and outputs (its private
         memory pool goes with them)."""
-        if self.graph is not None:
-            self.graph.reset()
-            self.graph, self.key, self.static, self.out = None, None, None, None
+        if self.graphs is not None:
+            for g in self.graphs:
+                g.reset()
+            self.graphs, self.reqs, self.key, self.static, self.out = None, [], None, None, None
             torch.cuda.empty_cache()
 
+    @property
+    def graph(self):
+        return self.graphs
+
     def _eager(self, batch):
-        return self.core(self.models, self.emas, self.optims, self.args, *batch)
+        return _drive(self.core(self.models, self.emas, self.optims, self.args, *batch))
+
+    def _replay(self):
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if i < len(self.reqs):
+                _collective(self.reqs[i])
+
+    def _capture(self, sbatch):
+        """Capture the step: one graph, or under torch.distributed one graph per
+        stretch between collectives (shared pool, replayed in this order)."""
+        gen = self.core(self.models, self.emas, self.optims, self.args, *sbatch)
+        keep = _KeepAll() if os.environ.get("UBPL_GRAPH_KEEPALL") == "1" else contextlib.nullcontext()
+        if not D.is_dist():
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g), keep:
+                self.out = _drive(gen)
+            self._kept = getattr(keep, "kept", None)
+            self.graphs, self.reqs = [g], []
+            return
+        pool = torch.cuda.graph_pool_handle()
+        graphs, reqs, done = [], [], False
+        while not done:
+            g = torch.cuda.CUDAGraph()
+            # thread_local: the process group's own threads may query HIP while a segment captures
+            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+                try:
+                    req = gen.send(None)
+                except StopIteration as e:
+                    self.out, done = e.value, True
+            graphs.append(g)
+            if not done:
+                reqs.append(req)
+        self.graphs, self.reqs = graphs, reqs
 
     def run(self, batch, dev):
         if not self.enabled or self._force_eager:
@@ -495,12 +633,12 @@ class _StepGraph:
         leaves = []
         spec = _flatten(batch, leaves)
         key = _spec_key(spec)
-        if self.graph is not None and key == self.key:
+        if self.graphs is not None and key == self.key:
             for dst, src in zip(self.static, leaves):
                 dst.copy_(src, non_blocking=True)
-            self.graph.replay()
+            self._replay()
             return self.out
-        if self.n_eager < self.WARM or self.graph is not None:
+        if self.n_eager < self.WARM or self.graphs is not None:
             # warm-up (or a batch of another shape): eager, on a side stream
             if self.side is None:
                 self.side = torch.cuda.Stream(device=dev)
@@ -514,21 +652,20 @@ class _StepGraph:
         self.static = [l.to(dev).clone() for l in leaves]
         sbatch = _unflatten(spec, self.static)
         torch.cuda.synchronize(dev)
-        g = torch.cuda.CUDAGraph()
-        keep = _KeepAll() if os.environ.get("UBPL_GRAPH_KEEPALL") == "1" else contextlib.nullcontext()
-        with torch.cuda.graph(g), keep:
-            self.out = self.core(self.models, self.emas, self.optims, self.args, *sbatch)
-        self._kept = getattr(keep, "kept", None)
-        self.graph, self.key = g, key
-        self.graph.replay()
+        self._capture(sbatch)
+        self.key = key
+        self._replay()
         return self.out
 
 
 def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, meta):
     """One MT_UBPL step (projects/MT_UBPL.py:188-336) on the device with no
-    host synchronisation: returns the packed records [3M+1 losses | counts |
-    pseudo scores] as ONE device tensor and the host-side constants needed to
-    unpack them.  Capturable in a HIP graph (see _StepGraph)."""
+    host synchronisation, as a generator: under torch.distributed it yields
+    its two exchanges (see _collective), and it returns the packed records
+    [3M+1 losses | counts | pseudo scores] as ONE device tensor and the
+    host-side constants needed to unpack them.  Run it with _drive (eager) or
+    _StepGraph (captured: one graph on one rank, one graph segment per
+    collective-free stretch under torch.distributed)."""
     M = len(models)
     dev = models[0].flat_params.device
     S = args.nStack
@@ -602,7 +739,13 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
     loc += _fdl_record_sums(fd)
     cn += [n[0] for _, _, n in fd]
     counts = torch.stack([c.float() for c in cn])
-    gcounts, gsums = _sync_stats(torch.stack([l.float() for l in loc]), counts)
+    local = torch.stack([l.float() for l in loc])
+    if D.is_dist():
+        pack = torch.cat([counts, local.detach()])
+        yield ("sum", pack)                                  # exchange 1: global sums / counts
+        gcounts, gsums = pack[:counts.numel()], pack[counts.numel():]
+    else:
+        gcounts, gsums = _sync_stats(local, counts)
     W = D.world()
     mtc_n = A * B * K * W
     nf = len(fd)
@@ -613,8 +756,11 @@ def _mt_ubpl_core(models, models_ema, optims, args, augs_imgMap, augs_heatmaps, 
         pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[3 * mi])
         epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[3 * mi + 1]) if use_ep else 0.
         totals.append(pec + mtc + epc + fdc)
-    _backward_all(totals, [t for grp in (outs, feats) for ts in grp for t in ts] if mstreams else None)   # :334-336
-    _join_and_allreduce(mstreams, models)
+    _backward_all(totals, [t for grp in (outs, feats) for ts in grp for t in ts] if mstreams else None,
+                  mstreams)                                                                    # :334-336
+    _join_merge(mstreams, models)
+    if D.is_dist():
+        yield ("grads", models)                              # exchange 2: SUM of the students' gradients
     _step_and_ema(models, models_ema, optims, args)
     # ---- records: one device->host copy
     g_rec = []
@@ -817,7 +963,7 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
                 pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[6 * mi + 1])
                 epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else 0.
                 totals.append(pec + mtc + epc + fdc)
-            _backward_all(totals, outs + feats if mstreams else None)   # DualPose_UBPL.py:277-279
+            _backward_all(totals, outs + feats if mstreams else None, mstreams)   # DualPose_UBPL.py:277-279
             _join_and_allreduce(mstreams, models)
             _step_and_ema(models, models_ema, optims, args)
             g_rec = []
