@@ -255,6 +255,17 @@ int64_t ubpl_wgrad3_psa_workspace(int B, int Cin, int Cout, int H, int W);
 int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int Cin,
                     int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,
                     void* stream);
+/* The 7x7 stride-2 stem's weight gradient (+ bias gradient, db nullable) on the
+ * split path, as the weight gradient of its space-to-depth form (replaces the
+ * exact-f32 ubpl_conv2d_wgrad for models/pose/hourglass.py pre.0 / layers.py:31-50):
+ * dys = split(dy) (PSA, pad 1, Cout channels at the H x W output), xs = the
+ * forward's phase image (ubpl_stem_s2d_split, 16 channels, pad 2); KS = 7, C <= 4
+ * input channels, Cout % 64 == 0, W % 16 == 0, npieces = 3.  _workspace: slab floats. */
+int64_t ubpl_wgrad_stem_psa_workspace(int B, int Cout, int H, int W);
+/*@ dys:u16[(npieces-1)*dplane+(int64_t)B*Cout*(H+2)*(W+2)] xs:u16[(npieces-1)*xplane+(int64_t)B*16*(H+4)*(W+4)] slab:f32[ubpl_wgrad_stem_psa_workspace(B,Cout,H,W)] dw:f32[(int64_t)Cout*C*KS*KS] db:f32[Cout] */
+int ubpl_wgrad_stem_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int C,
+                        int Cout, int H, int W, int KS, float* slab, float* dw, float* db, int accumulate,
+                        int npieces, void* stream);
 /* 1x1 weight gradient (+ bias gradient, db nullable) on the split path with
  * both f32 operands (dy [B,Cout,P], x [B,Cin,P], prologue relu(x*pscale +
  * pshift) when pscale != nullptr) split while staged: npieces 3 = 6xbf16,

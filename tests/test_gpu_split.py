@@ -553,6 +553,44 @@ def test_stem_s2d_vs_f64(B, H):
     assert esp <= max(2 * e32, 4 * 2.0 ** -24), (esp, e32)
 
 
+@pytest.mark.parametrize("B,H", [(2, 256), (4, 128), (32, 256)])
+def test_stem_weight_gradient_s2d_vs_f64(B, H):
+    """The stem's 7x7 stride-2 weight (+ bias) gradient as the weight gradient
+    of its space-to-depth 4x4 form on the split path (wgrad_stem_psa_kernel,
+    then the 4x4 -> 7x7 map), from PSA operands: split(dy) with a 1-pixel border
+    and the forward's phase image; within 2x the exact-f32 kernel's error vs
+    float64 (B=32, 256x256: the headline step's shape)."""
+    from ubpl_amd import kernels as Kn
+    gen = torch.Generator().manual_seed(37 + B + H)
+    x = torch.rand(B, 3, H, H, generator=gen) - 0.5
+    w = torch.randn(64, 3, 7, 7, generator=gen) / np.sqrt(147)
+    dy = torch.randn(B, 64, H // 2, H // 2, generator=gen)
+    d = lambda t: t.to(DEV)
+    sl = slice(0, min(B, 4))                        # the f64 reference over (up to) 4 images
+    xr, dyr = x[sl].double(), dy[sl].double()
+    wref = torch.nn.grad.conv2d_weight(xr, w.shape, dyr, stride=2, padding=3)
+    bref = dyr.sum((0, 2, 3))
+    xs, ys = Kn.stem_s2d_split(d(x[sl].contiguous()), 2), Kn.split_activation(d(dy[sl].contiguous()), 3, 1)
+    assert Kn.wgrad_stem_psa_ok(ys, xs, d(w))
+    dw, db = torch.full_like(d(w), 7.0), torch.full((64,), 7.0, device=DEV)
+    Kn.conv2d_wgrad_stem_psa(ys, xs, dw, db, accumulate=False)
+    dw32, db32 = torch.zeros_like(d(w)), torch.zeros(64, device=DEV)
+    Kn.conv2d_wgrad(d(dy[sl].contiguous()), d(x[sl].contiguous()), 7, 2, dw32, db32, accumulate=False)
+    e32, esp = _rel(dw32, wref), _rel(dw, wref)
+    eb32, ebsp = _rel(db32, bref), _rel(db, bref)
+    print("stem wgrad B=%d H=%d: f32 %.2e split %.2e | bias f32 %.2e split %.2e" % (B, H, e32, esp, eb32, ebsp))
+    assert esp <= max(2 * e32, 4 * 2.0 ** -24), (esp, e32)
+    assert ebsp <= max(2 * eb32, 4 * 2.0 ** -24), (ebsp, eb32)
+    # accumulate=True adds onto what is there
+    Kn.conv2d_wgrad_stem_psa(ys, xs, dw, db, accumulate=True)
+    assert _rel(dw, 2 * wref) <= max(2 * e32, 4 * 2.0 ** -24) + 1e-7
+    if B > 4:                                        # the full batch runs (the headline launch shape)
+        xs, ys = Kn.stem_s2d_split(d(x), 2), Kn.split_activation(d(dy), 3, 1)
+        Kn.conv2d_wgrad_stem_psa(ys, xs, dw, db, accumulate=False)
+        Kn.conv2d_wgrad(d(dy), d(x), 7, 2, dw32, db32, accumulate=False)
+        assert _rel(dw, dw32.cpu().double()) < 1e-5
+
+
 # the halo kernel's shapes (conv_psah_kernel: 3x3 pad 1, 128- / 64-row tiles, whole
 # rows of W = 32 / 64 / 128 per 256-pixel tile): (B, Cin, H, Cout)
 HALO_CASES = [(32, 128, 64, 128), (8, 128, 128, 128), (32, 256, 32, 256), (16, 256, 64, 256),

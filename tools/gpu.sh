@@ -29,6 +29,7 @@ cfg() { case $1 in head|eager) echo mt_ubpl;; hb) echo mt_ubpl_hg2_256_bf16;; c3
 envs() { [ -n "$1" ] && echo "${1//,/ }"; }
 stop() { echo "[$1] rc=$2: stopping"; exit $2; }
 
+nrun=0
 for step in "$@"; do
   kind=${step%%:*}; arg=${step#*:}; [ "$arg" = "$step" ] && arg=""
   name=${arg%%:*}; extra=${arg#*:}; [ "$extra" = "$arg" ] && extra=""
@@ -92,9 +93,10 @@ for step in "$@"; do
         done
       done ;;
     run)
-      cmd=${arg//+/ }
-      timeout -k 10 ${RUN_TIMEOUT:-300} $cmd > gpurun_out/run.log 2>&1
-      rc=$?; tail -${RUN_LINES:-30} gpurun_out/run.log; [ $rc -ne 0 ] && stop run $rc ;;
+      cmd=${arg//+/ }; nrun=$((nrun + 1))
+      timeout -k 10 ${RUN_TIMEOUT:-300} $cmd > gpurun_out/run$nrun.log 2>&1
+      rc=$?; echo "== run$nrun: $cmd"; grep -E "${RUN_GREP:-.}" gpurun_out/run$nrun.log | tail -${RUN_LINES:-30}
+      [ $rc -ne 0 ] && stop run $rc ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1178,7 +1178,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
 // BNT: pixels per tile, 256 (wave w: pixels 64w..64w+63) or 128 (32 per wave: half the
 // LDS and accumulators, three workgroups per CU, so one workgroup's epilogue stores run
 // beside the others' K loops)
-template <int BM, bool PRO, bool EPI = false, int NP = 3, int NS = 2, int BNT = 256>
+template <int BM, bool PRO, bool EPI = false, int NP = 3, int NS = 2, int BNT = 256, int NSB = NS>
 __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_kernel(const float* __restrict__ x,
                                                            const uint16_t* __restrict__ wp, int64_t wplane,
                                                            const float* __restrict__ bias,
@@ -1188,14 +1188,17 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
                                                            float* __restrict__ stat_part, ubpl::BnBwdEpi bwd) {
     // NP = 3: 6xbf16 (f32-equivalent); NP = 1: the "bf16" precision (operands
     // rounded to bf16, one MFMA per product, accumulated in f32 directly)
-    // NS: stages in the LDS ring (2, or 3 with 64-row tiles: two K steps' DMA in flight)
+    // NS: stages in the LDS ring (2, or 3 with 64-row tiles: two K steps' DMA in flight);
+    // NSB = 3 with NS = 2: a deeper ring for the activation stream alone (HBM: two K
+    // steps of it in flight per workgroup) beside the weights' two stages (L2-resident)
     static_assert(BNT == 256 || BNT == 128, "256- or 128-pixel tiles");
+    static_assert(NSB == NS || (NS == 2 && NSB == 3), "B ring: as deep as A's, or 3 beside A's 2");
     constexpr int TM = BM / 32, TN = BNT / 128;
     constexpr int BQ = BNT / 64;             // B DMA instructions per wave per K step (1 KB each)
     constexpr int AB = NP * BM * 32;         // A stage bytes: [piece][BM rows][32 B]
     constexpr int BH = 8 * BNT * 4 + 128;    // one 8-row half of the B image (+ bank shift)
     constexpr int BB = 2 * BH;
-    __shared__ __attribute__((aligned(16))) char lds[NS * (AB + BB)];
+    __shared__ __attribute__((aligned(16))) char lds[NS * AB + NSB * BB];   // A slots, then B slots
     // the prologue's (scale, shift) per input channel (K <= SOL_PRO_K), staged once:
     // a lane's 8 channels of a K step are 2 ds_read_b128 each, instead of scalar
     // loads of both 8-channel halves and 16 per-lane selects (48 VALU per K step)
@@ -1235,8 +1238,8 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         const int64_t b = n / P;
         b_lane = (uint32_t)((b * K * P + (n - b * P) + (BNT == 256 ? 0 : (int64_t)(lane >> 5) * P)) * 4);
     }
-    auto stage = [&](int buf, int kt) {
-        char* base = lds + buf * (AB + BB);
+    auto stage_a = [&](int buf, int kt) {
+        char* base = lds + buf * AB;
         if (a_issue) {
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
@@ -1245,13 +1248,20 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
                                                  (lds_ptr_t)(base + p * BM * 32 + wid * 1024), 16, 0, 0);
             }
         }
+    };
+    auto stage_b = [&](int buf, int kt) {
+        char* base = lds + NS * AB + buf * BB;
 #pragma unroll
         for (int q = 0; q < BQ; ++q) {
             const int r = 4 * wid + q * (4 / BQ);
             const char* bb = reinterpret_cast<const char*>(x + (int64_t)(kt + r) * P);
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
-                                             (lds_ptr_t)(base + AB + (r >> 3) * BH + (r & 7) * (BNT * 4)), 16, 0, 0);
+                                             (lds_ptr_t)(base + (r >> 3) * BH + (r & 7) * (BNT * 4)), 16, 0, 0);
         }
+    };
+    auto stage = [&](int buf, int kt) {
+        stage_a(buf, kt);
+        stage_b(buf, kt);
     };
 
     // accumulators start at bias (+ residual): see conv_psa_kernel
@@ -1284,22 +1294,34 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     ubpl::seed_acc<TM, TN>(acc, bias, tepi ? nullptr : res, obase, m0, M, P);
 
     const int nkt = K >> 4;
+    constexpr bool deepb = NSB != NS;
     stage(0, 0);
     if (NS == 3 && nkt > 1) stage(1, 16);
+    if (deepb && nkt > 1) stage_b(1, 16);
     for (int t = 0; t < nkt; ++t) {
         // stage t landed for every wave (NS = 3: this wave's stage t+1 DMA may stay in
-        // flight), every wave done with stage t-1
+        // flight; deepb: B(t+1), issued after A(t), may stay in flight), every wave
+        // done with stage t-1
         if (NS == 3 && t + 1 < nkt) {
             if (a_issue) vm_wait<NP + BQ>();
             else vm_wait<BQ>();
+        } else if (deepb && t + 1 < nkt) {
+            vm_wait<BQ>();
         } else {
             vm_wait<0>();
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (t + NS - 1 < nkt) stage((t + NS - 1) % NS, (t + NS - 1) * 16);
+        if (deepb) {
+            // A(t+1) first, then B(t+2): the next wait leaves only B(t+2) in flight
+            if (t + 1 < nkt) stage_a((t + 1) % NS, (t + 1) * 16);
+            if (t + 2 < nkt) stage_b((t + 2) % NSB, (t + 2) * 16);
+        } else if (t + NS - 1 < nkt) {
+            stage((t + NS - 1) % NS, (t + NS - 1) * 16);
+        }
         const int kt = t * 16;
-        const char* base = lds + (t % NS) * (AB + BB);
+        const char* base = lds + (t % NS) * AB;                       // A of stage t
+        const char* bbase = lds + NS * AB + (t % NSB) * BB;           // B of stage t
         // this lane's k half: 8 (scale, shift) pairs
         float sc[8], sh[8];
         if (PRO && !UBPL_SOL_LDS_COEF) {
@@ -1319,7 +1341,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
             sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
             sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
         }
-        const float* bs = reinterpret_cast<const float*>(base + AB + h * BH) + wn + li;
+        const float* bs = reinterpret_cast<const float*>(bbase + h * BH) + wn + li;
         bf16x8 bfr[TN][NP];
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -1415,7 +1437,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         // wave-private [32 rows][64 + 4 pixels] f32 image per 32-row block
         __syncthreads();
         constexpr int RS = 68;
-        static_assert(NS * (AB + BB) >= 4 * 32 * RS * 4, "transposed epilogue image exceeds the ring");
+        static_assert(NS * AB + NSB * BB >= 4 * 32 * RS * 4, "transposed epilogue image exceeds the ring");
         float* img = reinterpret_cast<float*>(lds) + wid * 32 * RS;
         const int rr = lane >> 4, c4 = (lane & 15) * 4;
         const int64_t n = n0 + wn + c4;   // 4 pixels of one image (P % 4 == 0)
@@ -1825,6 +1847,235 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa64_kernel(const uint16_t* __r
         const float v = bsum + __shfl_xor(bsum, 32, 64);
         if (h == 0) sl[(int64_t)(m0 + wm + li) * Nt + Ntot] = v;
     }
+}
+
+// ------------------------------------------------------------------ the stem's weight gradient (space-to-depth)
+// The 7x7 stride-2 stem's weight gradient as the weight gradient of its
+// space-to-depth form (stem_s2d_split_kernel / stem_weight_s2d_split_kernel): a
+// stride-1 4x4 conv of the 16-channel phase image, so
+//   dW'[co][tap (a, b)][ci] = sum over (n, oh, ow) of dy[n, co, oh, ow] * x'[n, ci, oh + a - 2, ow + b - 2]
+// on the split path, both operands PSA images: dys = split(dy) with a 1-pixel
+// border (the BN backward emits it), xs = the forward's phase image with its
+// 2-pixel border (kept for the backward).  GEMM: M = Cout (64-row blocks), N =
+// 16 taps x 16 channels (all of it per workgroup), K = pixels, K step = 16
+// consecutive pixels of one output row; split over workgroups into a slab
+// [z][Cout][257] reduced by wgrad_reduce_kernel (T = 16, Cin = 16; last column:
+// the bias gradient, from wave 0's A fragments).  Wave w takes kernel row a = w
+// (4 taps x 16 channels = 64 columns) x the 64 rows: wave tile 64 x 64.
+// Stage: A [piece][4 channel groups][16 px][32 B] (odd groups' pixel rows 0-3
+// <-> 4-7 swapped, as wgrad3_psa_kernel), B the 4-row x 19-pixel halo of the
+// step's receptive field [piece][4 rows][19 px][32 B] (a tap is a pixel offset);
+// fragments by ds_read_b64_tr_b16.  3-stage ring.
+template <int NP>
+__global__ void __launch_bounds__(NT, 2) wgrad_stem_psa_kernel(const uint16_t* __restrict__ dys, int64_t dplane,
+                                                              const uint16_t* __restrict__ xs, int64_t xplane,
+                                                              int B, int Cout, int H, int W, int steps_per_split,
+                                                              float* __restrict__ slab) {
+    constexpr int NS = 3, HXP = 19, BROWS = 4 * HXP;       // halo: 4 rows x 19 pixels
+    constexpr int API = 4 * 16 * 32;                       // A piece image: 4 groups x 16 px x 32 B
+    constexpr int BPI = BROWS * 32;                        // B piece image
+    constexpr int AB = NP * API, SUB = AB + NP * BPI;
+    constexpr int AI = NP * 2, BI = NP * 3, NI = AI + BI;  // DMA instructions per stage (1 KB each)
+    constexpr int NPW = (NI + 3) / 4;                      // per wave
+    __shared__ __attribute__((aligned(16))) char lds[NS * SUB];
+    typedef short v4i16 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4i16* tr_ptr_t;
+
+    const int Hp = H + 2, Wp = W + 2, Hx = H + 4, Wx = W + 4;
+    const int Go = Cout >> 4;
+    constexpr int Ntot = 256, Nt = Ntot + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    static_assert(NP == 3, "6xbf16 operands");
+    // grid (Cout / 64, splits): the row blocks of one split side by side (same L2)
+    const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    const int by = lam % gridDim.x, bz = lam / gridDim.x;
+    const int m0 = by * 64;
+    const int wsteps = W >> 4;
+    const int total_steps = B * H * wsteps;
+    const int s_begin = bz * steps_per_split;
+    const int s_end = min(total_steps, s_begin + steps_per_split);
+    const int nkt = max(0, s_end - s_begin);
+
+    // per-instruction lane offsets (bytes, relative to the step's base): instruction i
+    // of a stage, i = u * 4 + wid: A piece i / 2 (groups 2 (i % 2), +1), B piece
+    // (i - AI) / 3, 32-pixel chunk (i - AI) % 3 (the last one overlapping: starts at 76 - 32)
+    uint32_t loff[NPW];
+    int lpiece[NPW];
+    bool lisa[NPW], lon[NPW];
+    const int lrow = lane >> 1, lhalf = lane & 1;
+#pragma unroll
+    for (int u = 0; u < NPW; ++u) {
+        const int i = u * 4 + wid;
+        lon[u] = i < NI;
+        lisa[u] = i < AI;
+        if (i < AI) {
+            const int gl = 2 * (i % 2) + (lrow >> 4);
+            const int rphys = lrow & 15, rlog = rphys ^ (4 * (gl & 1));
+            lpiece[u] = i / 2;
+            loff[u] = (uint32_t)((((int64_t)gl * Hp * Wp) + rlog) * 16 + 8 * lhalf) * 2;
+        } else {
+            const int j = i - AI, c = j % 3;
+            const int q = min(c * 32, BROWS - 32) + lrow;
+            const int a = q / HXP, px = q - a * HXP;
+            lpiece[u] = j / 3;
+            loff[u] = (uint32_t)(((int64_t)a * Wx + px) * 16 + 8 * lhalf) * 2;
+        }
+    }
+    const char* dys_m = reinterpret_cast<const char*>(dys + (int64_t)(m0 >> 4) * Hp * Wp * 16);
+    auto stage = [&](int buf, int s) {
+        if (s >= s_end) return;
+        const int b = s / (H * wsteps);
+        const int rem = s - b * (H * wsteps);
+        const int oh = rem / wsteps, ow0 = (rem - oh * wsteps) * 16;
+        const int64_t aoff = ((int64_t)b * Go * Hp * Wp + (int64_t)(oh + 1) * Wp + ow0 + 1) * 16;
+        const int64_t boff = (((int64_t)b * Hx + oh) * Wx + ow0) * 16;
+        char* base = lds + buf * SUB;
+#pragma unroll
+        for (int u = 0; u < NPW; ++u) {
+            if (!lon[u]) continue;
+            const int i = u * 4 + wid;
+            if (lisa[u]) {
+                const char* src = dys_m + 2 * (lpiece[u] * dplane + aoff);
+                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + loff[u]),
+                                                 (lds_ptr_t)(base + lpiece[u] * API + (i % 2) * 1024), 16, 0, 0);
+            } else {
+                const int j = i - AI, c = j % 3;
+                const char* src = reinterpret_cast<const char*>(xs) + 2 * (lpiece[u] * xplane + boff);
+                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + loff[u]),
+                                                 (lds_ptr_t)(base + AB + lpiece[u] * BPI + min(c * 32, BROWS - 32) * 32),
+                                                 16, 0, 0);
+            }
+        }
+    };
+    // this wave's DMA instructions per stage (the counted waits below)
+    const int mine = (NI - wid + 3) / 4;
+
+    // transposed reads: 16-lane group g16 = lane >> 4; lane i16 = (qrow, pcol)
+    const int g16 = lane >> 4, i16 = lane & 15;
+    const int qrow = i16 >> 2, pcol = i16 & 3;
+    int aoffs[2][2], boffs[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int grp = 2 * i + (g16 & 1);
+            const int row = (8 * (g16 >> 1) + 4 * t + qrow) ^ (4 * (grp & 1));
+            aoffs[i][t] = grp * 512 + row * 32 + 8 * pcol;
+        }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int px = 8 * (g16 >> 1) + 4 * t + qrow + 2 * j + (g16 & 1);   // tap b = 2j + (g16 & 1)
+            boffs[j][t] = (wid * HXP + px) * 32 + 8 * pcol;
+        }
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const bool bias_wave = wid == 0;
+    float bsum[2] = {0.f, 0.f};
+
+    stage(0, s_begin);
+    stage(1, s_begin + 1);
+    for (int t = 0; t < nkt; ++t) {
+        // stage t landed (this wave's stage t+1 DMA may stay in flight)
+        if (t + 1 < nkt) {
+            if (mine == 4) vm_wait<4>();   // (NP = 3: 15 instructions per stage, 4 / 4 / 4 / 3 per wave)
+            else vm_wait<3>();
+        } else {
+            vm_wait<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (t + 2 < nkt) stage((t + 2) % NS, s_begin + t + 2);
+        char* base = lds + (t % NS) * SUB;
+        bf16x8 af[2][NP], bfr[2][NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * API + aoffs[i][0]));
+                const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + p * API + aoffs[i][1]));
+                const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                af[i][p] = __builtin_bit_cast(bf16x8, v);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * BPI + boffs[j][0]));
+                const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr_t)(base + AB + p * BPI + boffs[j][1]));
+                const short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                bfr[j][p] = __builtin_bit_cast(bf16x8, v);
+            }
+        }
+        if (bias_wave) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int p = 0; p < NP; ++p)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) bsum[i] += (float)af[i][p][e];
+        }
+        floatx16 tmp[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) tmp[i][j] = mfma_split0<NP>(af[i], bfr[j]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) drain(acc[i][j], tmp[i][j]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    float* sl = slab + (int64_t)bz * Cout * Nt;
+    const int li = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = 64 * wid + 32 * j + li;                   // tap 4 wid + 2 j + li / 16, channel li % 16
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                sl[(int64_t)m * Nt + n] = acc[i][j][r];
+            }
+    }
+    if (bias_wave) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            // lane (r, h) summed channel 32i + r over pixels 8h..8h+7 of each step
+            const float v = bsum[i] + __shfl_xor(bsum[i], 32, 64);
+            if (h == 0) sl[(int64_t)(m0 + 32 * i + li) * Nt + Ntot] = v;
+        }
+    }
+}
+
+// the space-to-depth weight gradient dws [Cout][16 ci][16 taps] + its bias column dbs
+// [Cout] (wgrad_reduce_kernel's layout for Cin = 16, T = 16) -> the 7x7 gradient dw
+// [Cout][C][7][7] (+)= and db (+)=: tap (a, b), channel c*4 + 2 ph + pw of the phase
+// image holds w[.][c][2 (a - 2) + ph + 3][2 (b - 2) + pw + 3], i.e. kh -> (ph, a) =
+// ((kh + 1) & 1, (kh + 1 - ph) / 2)
+__global__ void __launch_bounds__(256) stem_wgrad_map_kernel(const float* __restrict__ dws,
+                                                             const float* __restrict__ dbs, int Cout, int C,
+                                                             float* __restrict__ dw, float* __restrict__ db,
+                                                             int accumulate) {
+    constexpr int KS = 7;
+    const int64_t total = (int64_t)Cout * C * KS * KS;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (db != nullptr && idx < Cout) db[idx] = accumulate ? db[idx] + dbs[idx] : dbs[idx];
+    if (idx >= total) return;
+    const int kw = (int)(idx % KS), kh = (int)((idx / KS) % KS);
+    const int c = (int)((idx / (KS * KS)) % C), o = (int)(idx / (KS * KS * C));
+    const int ph = (kh + 1) & 1, a = (kh + 1 - ph) / 2;
+    const int pw = (kw + 1) & 1, bb = (kw + 1 - pw) / 2;
+    const float v = dws[(int64_t)o * 256 + (c * 4 + 2 * ph + pw) * 16 + a * 4 + bb];
+    dw[idx] = accumulate ? dw[idx] + v : v;
 }
 
 // ------------------------------------------------------------------ 1x1 weight gradient, split on load
@@ -2631,13 +2882,20 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     const bool epi = stat_part != nullptr || bn_part != nullptr;
     if (epi && (npieces == 1 || Cout % 64 != 0)) return (int)hipErrorInvalidValue;   // (epilogue partials: 6xbf16, whole tiles)
     static const bool ns3 = sol_env("UBPL_SOL_NS", 2) == 3;
+    // the activation ring 3 stages deep beside the weights' 2 (two K steps of the HBM
+    // stream in flight per workgroup); UBPL_SOL_NSB=2: one ring of 2 stages (round 4)
+    static const bool nsb3 = sol_env("UBPL_SOL_NSB", 3) == 3;
     // UBPL_SOL_BN=128: 128-pixel tiles (three workgroups per CU) on the 6xbf16 path
-    const bool bn128 = sol_env("UBPL_SOL_BN", 256) == 128 && npieces == 3 && !epi && N % 128 == 0;
+    static const bool bn128_env = sol_env("UBPL_SOL_BN", 256) == 128;
+    const bool bn128 = bn128_env && npieces == 3 && !epi && N % 128 == 0;
     const dim3 grid128((unsigned)(N / 128), (unsigned)((Cout + bm - 1) / bm));
 #define UBPL_SOL(BM_, PRO_)                                                                                       \
     do {                                                                                                          \
         if (bn128)                                                                                                \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 3, 2, 128>), grid128, dim3(NT), 0, st, x,    \
+                               wsplit, wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);      \
+        else if (npieces == 1 && nsb3)                                                                            \
+            hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 1, 2, 256, 3>), grid, dim3(NT), 0, st, x,    \
                                wsplit, wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);      \
         else if (npieces == 1)                                                                                    \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 1>), grid, dim3(NT), 0, st, x, wsplit,       \
@@ -2648,6 +2906,9 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
         else if (epi)                                                                                             \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, true>), grid, dim3(NT), 0, st, x, wsplit, wplane,   \
                                bias, pscale, pshift, res, y, B, Cin, P, Cout, stat_part, bwd);                    \
+        else if (nsb3)                                                                                            \
+            hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 3, 2, 256, 3>), grid, dim3(NT), 0, st, x,    \
+                               wsplit, wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);      \
         else                                                                                                      \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_>), grid, dim3(NT), 0, st, x, wsplit, wplane, bias,   \
                                pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);                            \
@@ -2721,6 +2982,47 @@ UBPL_API int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t
     }
     UBPL_LAUNCH_CHECK();
     return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 9, db != nullptr, dw, db, accumulate, stream);
+}
+
+// ---- the stem's weight gradient on the split path (space-to-depth)
+namespace {
+int wgrad_stem_splits(int B, int Cout, int H, int W) {
+    const int steps = B * H * (W / 16);
+    int s = 512 / (Cout / 64);                          // one round of 2 workgroups per CU
+    if (s < 1) s = 1;
+    if (s > steps / 8) s = steps / 8 > 0 ? steps / 8 : 1;
+    const int per = (steps + s - 1) / s;
+    return (steps + per - 1) / per;
+}
+}  // namespace
+
+UBPL_API int64_t ubpl_wgrad_stem_psa_workspace(int B, int Cout, int H, int W) {
+    if (B < 1 || Cout % 64 || W % 16 || H < 1) return 0;
+    return (int64_t)wgrad_stem_splits(B, Cout, H, W) * Cout * 257 + (int64_t)Cout * 257;
+}
+
+UBPL_API int ubpl_wgrad_stem_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B,
+                                 int C, int Cout, int H, int W, int KS, float* slab, float* dw, float* db,
+                                 int accumulate, int npieces, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (npieces != 3 || KS != 7 || C < 1 || C > 4 || Cout % 64 || W % 16 || H < 1 || B < 1 || slab == nullptr)
+        return (int)hipErrorInvalidValue;
+    if ((((uintptr_t)dys) & 15) || (((uintptr_t)xs) & 15) || (dplane % 8) || (xplane % 8))
+        return (int)hipErrorInvalidValue;
+    const int splits = wgrad_stem_splits(B, Cout, H, W);
+    const int steps = B * H * (W / 16);
+    const int per = (steps + splits - 1) / splits;
+    hipLaunchKernelGGL((wgrad_stem_psa_kernel<3>), dim3((unsigned)(Cout / 64), (unsigned)splits), dim3(NT), 0, st,
+                       dys, dplane, xs, xplane, B, Cout, H, W, per, slab);
+    UBPL_LAUNCH_CHECK();
+    float* dws = slab + (int64_t)splits * Cout * 257;
+    const int e = ubpl_wgrad_slab_reduce(slab, splits, Cout, 16, 16, 1, dws, dws + (int64_t)Cout * 256, 0, stream);
+    if (e) return e;
+    const int64_t total = (int64_t)Cout * C * KS * KS;
+    hipLaunchKernelGGL(stem_wgrad_map_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dws,
+                       dws + (int64_t)Cout * 256, Cout, C, dw, db, accumulate);
+    UBPL_LAUNCH_CHECK();
+    return 0;
 }
 
 // ---- 1x1 weight gradient with the split on load

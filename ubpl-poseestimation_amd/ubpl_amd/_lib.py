@@ -61,6 +61,8 @@ SIGNATURES = {
     "ubpl_wgrad_slab_reduce": (I, [P, I, I, I, I, I, P, P, I, P]),
     "ubpl_wgrad3_psa_workspace": (L, [I, I, I, I, I]),
     "ubpl_wgrad3_psa": (I, [P, L, P, L, I, I, I, I, I, P, P, P, I, I, P]),
+    "ubpl_wgrad_stem_psa_workspace": (L, [I, I, I, I]),
+    "ubpl_wgrad_stem_psa": (I, [P, L, P, L, I, I, I, I, I, I, P, P, P, I, I, P]),
     "ubpl_wgrad1x1_split_load_workspace": (L, [I, I, I, I]),
     "ubpl_wgrad1x1_split_load": (I, [P, P, I, I, I, I, P, P, P, P, P, I, I, P]),
     "ubpl_conv2d_forward_split_workspace": (L, [I, I, I, I, I, I, I]),

@@ -43,6 +43,9 @@ _WGRAD1_SPLIT = os.environ.get("UBPL_WGRAD1_SPLIT", "1") != "0"
 _BWD_EPI = os.environ.get("UBPL_BWD_EPI", "0") == "1"
 # the 7x7/s2 stem on the split path by space-to-depth (UBPL_STEM_S2D=0: exact-f32 kernel)
 _STEM_S2D = os.environ.get("UBPL_STEM_S2D", "1") != "0"
+# the stem's 7x7 weight gradient on the split path from the forward's space-to-depth image
+# (round 5; UBPL_STEM_WGRAD=0: the exact-f32 conv_wgrad2_kernel)
+_STEM_WGRAD = os.environ.get("UBPL_STEM_WGRAD", "1") != "0"
 # forward BatchNorm statistics from the conv epilogues (UBPL_FWD_EPI=1).  Off by default:
 # epilogue partials + a finalize launch measured 1.3 % slower than the one-launch
 # statistics pass (stats_kernel) on the training step.
@@ -631,7 +634,10 @@ class _Exec:
         if self.m.conv_pieces == 3 and _STEM_S2D and Kn.stem_s2d_ok(imgs):
             # 7x7/s2 as a 4x4 stride-1 conv over the space-to-depth image, on the split path
             ws = Kn.stem_weight_s2d_split(self.m.P("pre.0.conv.weight"))
-            y0 = Kn.conv2d_forward_psa(Kn.stem_s2d_split(imgs, 2), ws, self.m.P("pre.0.conv.bias"))
+            xs = Kn.stem_s2d_split(imgs, 2)
+            y0 = Kn.conv2d_forward_psa(xs, ws, self.m.P("pre.0.conv.bias"))
+            if self.do_save and _STEM_WGRAD:
+                self.saved_split["pre.0.conv"] = xs      # the weight gradient's B operand
         else:
             y0 = self.conv("pre.0.conv", imgs, stride=2)
         sc, sh = self.bn("pre.0.bn", y0)
@@ -847,6 +853,17 @@ class _Exec:
         Kn.maxpool2x2_backward(x1, d, dx1, accumulate=False)
         d = self.residual_bwd("pre.1", dx1)
         imgs, y0 = self.saved.get("pre.0")
+        xs = self.saved_split.get("pre.0.conv")
+        w0 = m.P("pre.0.conv.weight")
+        if xs is not None and m.conv_pieces == 3 and d.shape[1] % 64 == 0 and d.shape[3] % 16 == 0:
+            # dy of the stem only as the split operand of its weight gradient (the input
+            # image takes no gradient): the space-to-depth 4x4 weight gradient, mapped to 7x7
+            ys = self.bn_bwd_split("pre.0.bn", d, y0, relu=1)
+            if Kn.wgrad_stem_psa_ok(ys, xs, w0):
+                Kn.conv2d_wgrad_stem_psa(ys, xs, self.G("pre.0.conv.weight"), self.G("pre.0.conv.bias"))
+                return
+            raise RuntimeError("ubpl_amd: stem weight gradient operands %s / %s" % (
+                (ys.B, ys.C, ys.H, ys.W, ys.pad), (xs.B, xs.C, xs.H, xs.W, xs.pad)))
         d = self.bn_bwd("pre.0.bn", d, y0, relu=1)
         self.wgrad("pre.0.conv", d, imgs, 7, stride=2)
 

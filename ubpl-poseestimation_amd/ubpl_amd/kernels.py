@@ -572,6 +572,23 @@ def conv2d_wgrad3_psa(ys, xs, dw, db, accumulate=True):
          _p(slab), _p(dw), _p(db), int(accumulate), int(xs.npieces))
 
 
+def wgrad_stem_psa_ok(ys, xs, w):
+    Cout, C, KS = w.shape[0], w.shape[1], w.shape[2]
+    return (ys.npieces == 3 and xs.npieces == 3 and ys.pad == 1 and xs.pad == 2 and xs.C == 16 and KS == 7
+            and C <= 4 and Cout % 64 == 0 and ys.C == Cout and ys.W % 16 == 0
+            and (ys.B, ys.H, ys.W) == (xs.B, xs.H, xs.W))
+
+
+def conv2d_wgrad_stem_psa(ys, xs, dw, db, accumulate=True):
+    """The 7x7/s2 stem's weight (+ bias) gradient from PSA operands: ys = split(dy) (pad 1),
+    xs = the forward's space-to-depth phase image (stem_s2d_split, pad 2)."""
+    Cout, C, KS = dw.shape[0], dw.shape[1], dw.shape[2]
+    n = _lib.lib().ubpl_wgrad_stem_psa_workspace(ys.B, Cout, ys.H, ys.W)
+    slab = torch.empty(int(n), device=ys.buf.device, dtype=F32)
+    call("ubpl_wgrad_stem_psa", _p(ys.buf), int(ys.plane), _p(xs.buf), int(xs.plane), ys.B, C, Cout, ys.H, ys.W, KS,
+         _p(slab), _p(dw), _p(db), int(accumulate), 3)
+
+
 def conv2d_dgrad(dy, w, res=None, out=None, wt=None):
     """dx of a stride-1 conv = conv(dy, flip(w)^T); res/out allow accumulation."""
     if wt is None:
