@@ -19,6 +19,7 @@
 // dx = a*dyp + b*(x - mean) + c with a = g*invstd, b = -g*invstd^3*S2/N,
 // c = -g*invstd*S1/N, plus up to two addends (residual-gradient sums).
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -459,6 +460,46 @@ __global__ void __launch_bounds__(256) bwd_apply_vec_kernel(const float* dz, con
     }
 }
 
+// The same per (image, channel) plane (HW4 % 256 == 0: planes of 32x32 and up): grid
+// (HW4 / (256 U), B*C), so the channel and its six coefficients are block-uniform (scalar
+// loads, no per-element 64-bit index division) and each thread issues its U float4s of
+// every operand before computing (dx may alias dz / add1 / add2: same elements).
+template <int U>
+__global__ void __launch_bounds__(256) bwd_apply_plane_kernel(const float* dz, const float* __restrict__ x, int C,
+                                                             int HW4, const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean, int relu,
+                                                             const float* __restrict__ ca,
+                                                             const float* __restrict__ cb,
+                                                             const float* __restrict__ cc, const float* add1,
+                                                             const float* add2, float* dx) {
+    const int pl = blockIdx.y;
+    const int c = pl % C;
+    const float sc = scale[c], sh = shift[c], mu = mean[c], a = ca[c], b = cb[c], cx = cc[c];
+    const int64_t base = (int64_t)pl * HW4 + blockIdx.x * (256 * U) + threadIdx.x;
+    const float4* x4 = reinterpret_cast<const float4*>(x) + base;
+    const float4* d4 = reinterpret_cast<const float4*>(dz) + base;
+    float4 xv[U], g[U], q1[U], q2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        xv[u] = x4[u * 256];
+        g[u] = d4[u * 256];
+        if (add1) q1[u] = reinterpret_cast<const float4*>(add1)[base + u * 256];
+        if (add2) q2[u] = reinterpret_cast<const float4*>(add2)[base + u * 256];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        float4 v;
+        v.x = bwd_one(g[u].x, xv[u].x, sc, sh, mu, a, b, cx, relu);
+        v.y = bwd_one(g[u].y, xv[u].y, sc, sh, mu, a, b, cx, relu);
+        v.z = bwd_one(g[u].z, xv[u].z, sc, sh, mu, a, b, cx, relu);
+        v.w = bwd_one(g[u].w, xv[u].w, sc, sh, mu, a, b, cx, relu);
+        if (add1) { v.x += q1[u].x; v.y += q1[u].y; v.z += q1[u].z; v.w += q1[u].w; }
+        if (add2) { v.x += q2[u].x; v.y += q2[u].y; v.z += q2[u].z; v.w += q2[u].w; }
+        reinterpret_cast<float4*>(dx)[base + u * 256] = v;
+    }
+}
+
 __global__ void __launch_bounds__(256) bwd_apply_kernel(const float* dz, const float* __restrict__ x, int C, int HW,
                                                        int64_t total, const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
@@ -809,7 +850,25 @@ UBPL_API int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int
     const bool vec = (HW % 4 == 0) && ((al & 15) == 0);
     const float *ca = coef, *cb = coef + C, *cc = coef + 2 * C;
     const int64_t total = (int64_t)B * C * HW;
-    if (vec)
+    // (UBPL_BN_PLANE=0: the round-4 grid-stride kernel everywhere)
+    static const bool plane_env = [] {
+        const char* e = getenv("UBPL_BN_PLANE");
+        return !(e && atoi(e) == 0);
+    }();
+    const int hw4 = HW / 4;
+    if (vec && plane_env && hw4 % 256 == 0 && (int64_t)B * C < 65536) {
+        const int u = hw4 % 1024 == 0 ? 4 : (hw4 % 512 == 0 ? 2 : 1);
+        const dim3 grid((unsigned)(hw4 / (256 * u)), (unsigned)(B * C));
+        if (u == 4)
+            hipLaunchKernelGGL(bwd_apply_plane_kernel<4>, grid, dim3(256), 0, st, dz, x, C, hw4, scale, shift, mean,
+                               relu, ca, cb, cc, add1, add2, dx);
+        else if (u == 2)
+            hipLaunchKernelGGL(bwd_apply_plane_kernel<2>, grid, dim3(256), 0, st, dz, x, C, hw4, scale, shift, mean,
+                               relu, ca, cb, cc, add1, add2, dx);
+        else
+            hipLaunchKernelGGL(bwd_apply_plane_kernel<1>, grid, dim3(256), 0, st, dz, x, C, hw4, scale, shift, mean,
+                               relu, ca, cb, cc, add1, add2, dx);
+    } else if (vec)
         hipLaunchKernelGGL(bwd_apply_vec_kernel, dim3(grid_ew(total / 4)), dim3(256), 0, st, dz, x, C, HW / 4,
                            total / 4, scale, shift, mean, relu, ca, cb, cc, add1, add2, dx);
     else
