@@ -1492,6 +1492,255 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     store_tile<TM, TN>(acc, nok, obase, m0, M, P, y, m0 + BM <= M && n0 + BNT <= N);
 }
 
+// ------------------------------------------------------------------ 1x1, split on load, warp-specialized (round 5)
+// conv1x1_sol_kernel's arithmetic (y = W v + bias (+ res), v = relu(x*pscale + pshift)
+// or x, NP bf16 pieces per operand, 16-k chunks drained into f32 accumulators) with the
+// split taken off the MFMA waves: 512 threads, 4 MFMA waves (wave w: all 128 rows x
+// pixels 64w..64w+63 of the 256-pixel tile, as conv1x1_sol_kernel) and 4 loader waves.
+// The loader waves stream the operands by LDS-DMA — weights [piece][128 rows][32 B]
+// (3-slot ring, two K steps ahead), activations as f32 rows [16 k][256 px] (3-slot
+// ring, three K steps ahead) — and, one K step ahead of the MFMA waves, read the f32
+// image (thread = pixel: 16 ds_read_b32), apply the BN+ReLU prologue, split into NP
+// bf16 pieces and write them as the MFMA-ready image [piece][256 px][32 B] (chunk
+// swizzled by (px >> 3) & 1; 2-slot ring).  One s_barrier per K step for all eight
+// waves; a loader wave waits (counted vmcnt) for its own DMA of the next step's
+// operands before it.  The MFMA waves issue only fragment reads, MFMAs and the chunk
+// drains; the VALU of the split runs beside them on the loader waves of the same SIMD.
+// Persistent: one workgroup per CU walks tiles L, L + G, ... (L the XCD-remapped block
+// index), the step stream (tile, k) flattened, so the rings run across tile boundaries
+// and a tile's epilogue stores overlap the next tile's operand DMA.
+template <int NP, bool PRO>
+__global__ void __launch_bounds__(2 * NT, 1) conv1x1_ws_kernel(const float* __restrict__ x,
+                                                              const uint16_t* __restrict__ wp, int64_t wplane,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ pscale,
+                                                              const float* __restrict__ pshift, const float* res,
+                                                              float* y, int B, int K, int P, int M, int ntiles) {
+    constexpr int BM = 128, BNT = 256, TM = 4, TN = 2;
+    constexpr int AB = NP * BM * 32;                // A stage: [piece][128 rows][32 B]
+    constexpr int BH = 8 * BNT * 4 + 128;           // f32 B stage half: 8 k rows (+ bank shift)
+    constexpr int BB = 2 * BH;
+    constexpr int PB = NP * BNT * 32;               // pieces stage: [piece][256 px][32 B]
+    constexpr int NSA = 3, NSB = 3, NSP = 2;
+    constexpr int OFF_B = NSA * AB, OFF_P = OFF_B + NSB * BB;
+    static_assert(OFF_P + NSP * PB <= 160 * 1024 - 2 * 4 * SOL_PRO_K, "LDS");
+    __shared__ __attribute__((aligned(16))) char lds[OFF_P + NSP * PB];
+    __shared__ __attribute__((aligned(16))) float lds_sc[PRO ? SOL_PRO_K : 4], lds_sh[PRO ? SOL_PRO_K : 4];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool loader = wid >= 4;
+    const int lw = wid & 3;
+    if (PRO) {
+        for (int k = tid; k < K; k += 2 * NT) {
+            lds_sc[k] = pscale[k];
+            lds_sh[k] = pshift[k];
+        }
+        __syncthreads();
+    }
+    const int64_t N = (int64_t)B * P;
+    const int nkt = K >> 4;
+    const int gy = (M + BM - 1) / BM;
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int my_tiles = L < ntiles ? (ntiles - L + gridDim.x - 1) / gridDim.x : 0;
+    const int nsteps = my_tiles * nkt;
+    auto tile_of = [&](int s, int& m0, int64_t& n0) {
+        const int tl = L + (s / nkt) * gridDim.x;
+        m0 = (tl % gy) * BM;
+        n0 = (int64_t)(tl / gy) * BNT;
+    };
+
+    // ---- loader side: DMA and split
+    const int lr = lane >> 1;
+    const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
+    auto stage_a = [&](int s) {
+        int m0;
+        int64_t n0;
+        tile_of(s, m0, n0);
+        const int kt = (s % nkt) * 16;
+        const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * lw + lr, M - 1) * K + 8 * lchunk) * 2);
+        char* base = lds + (s % NSA) * AB;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            const char* ab = reinterpret_cast<const char*>(wp + p * wplane + kt);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane), (lds_ptr_t)(base + p * BM * 32 + lw * 1024), 16,
+                                             0, 0);
+        }
+    };
+    auto stage_b = [&](int s) {
+        int m0;
+        int64_t n0;
+        tile_of(s, m0, n0);
+        const int kt = (s % nkt) * 16;
+        int64_t n = n0 + 4 * lane;
+        n = n < N ? n : N - 4;
+        const int64_t b = n / P;
+        const uint32_t b_lane = (uint32_t)((b * K * P + (n - b * P)) * 4);
+        char* base = lds + OFF_B + (s % NSB) * BB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = 4 * lw + q;
+            const char* bb = reinterpret_cast<const char*>(x + (int64_t)(kt + r) * P);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
+                                             (lds_ptr_t)(base + (r >> 3) * BH + (r & 7) * (BNT * 4)), 16, 0, 0);
+        }
+    };
+    // thread (tid - 256) = pixel px of the tile: 16 k values -> NP pieces, 2 x 16 B each
+    auto split_step = [&](int s) {
+        const int px = tid - 2 * 128;
+        const int kt = (s % nkt) * 16;
+        const float* bimg = reinterpret_cast<const float*>(lds + OFF_B + (s % NSB) * BB);
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = bimg[(k >> 3) * (BH / 4) + (k & 7) * BNT + px];
+        if (PRO) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = fmaxf(fmaf(v[k], lds_sc[kt + k], lds_sh[kt + k]), 0.f);
+        }
+        uint32_t pk[NP][8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            uint32_t o[NP];
+            split2<NP>(v[2 * e], v[2 * e + 1], o);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) pk[p][e] = o[p];
+        }
+        char* pb = lds + OFF_P + (s % NSP) * PB + px * 32;
+        const int sw = (px >> 3) & 1;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            *reinterpret_cast<uint4*>(pb + p * (BNT * 32) + 16 * (0 ^ sw)) = make_uint4(pk[p][0], pk[p][1], pk[p][2], pk[p][3]);
+            *reinterpret_cast<uint4*>(pb + p * (BNT * 32) + 16 * (1 ^ sw)) = make_uint4(pk[p][4], pk[p][5], pk[p][6], pk[p][7]);
+        }
+    };
+    // this loader wave's outstanding DMA instructions allowed when A(s+1), B(s+2) must
+    // have landed: A(s+2) (NP) and B(s+3) (4), when issued
+    auto loader_wait = [&](int s) {
+        const bool a2 = s + 2 < nsteps, b3 = s + 3 < nsteps;
+        if (a2 && b3) vm_wait<NP + 4>();
+        else if (a2) vm_wait<NP>();
+        else vm_wait<0>();
+    };
+
+    if (loader) {
+        // prologue: A(0), B(0), A(1), B(1), B(2); then A(0), B(0) landed
+        if (nsteps > 0) { stage_a(0); stage_b(0); }
+        if (nsteps > 1) { stage_a(1); stage_b(1); }
+        if (nsteps > 2) stage_b(2);
+        if (nsteps > 2) vm_wait<NP + 8>();
+        else if (nsteps > 1) vm_wait<NP + 4>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();      // every loader's part of B(0) landed
+        asm volatile("" ::: "memory");
+        if (nsteps > 0) {
+            split_step(0);
+            // before barrier(0): B(1) landed (A(1) with it; B(2) may stay in flight)
+            if (nsteps > 2) vm_wait<4>();
+            else vm_wait<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        for (int s = 0; s < nsteps; ++s) {
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (s + 2 < nsteps) stage_a(s + 2);
+            if (s + 3 < nsteps) stage_b(s + 3);
+            if (s + 1 < nsteps) split_step(s + 1);
+            loader_wait(s);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        return;
+    }
+
+    // ---- MFMA waves (the same barriers, one per step): per tile, seed / K loop / epilogue
+    const int li = lane & 31, h = lane >> 5;
+    const int wn = 64 * lw;
+    __builtin_amdgcn_s_barrier();          // the prologue barrier
+    asm volatile("" ::: "memory");
+    for (int it = 0; it < my_tiles; ++it) {
+        int m0;
+        int64_t n0;
+        tile_of(it * nkt, m0, n0);
+        floatx16 acc[TM][TN];
+        if (bias != nullptr) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float bv = bias[min(m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1)];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j][r] = bv;
+                }
+        } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        }
+        for (int t = 0; t < nkt; ++t) {
+            const int s = it * nkt + t;
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const char* abase = lds + (s % NSA) * AB;
+            const char* pbase = lds + OFF_P + (s % NSP) * PB;
+            bf16x8 bfr[TN][NP];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int px = wn + 32 * j + li;
+#pragma unroll
+                for (int p = 0; p < NP; ++p)
+                    bfr[j][p] = *reinterpret_cast<const bf16x8*>(pbase + p * (BNT * 32) + px * 32 +
+                                                                  16 * (h ^ ((px >> 3) & 1)));
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int row = 32 * i + li;
+                bf16x8 af[NP];
+#pragma unroll
+                for (int p = 0; p < NP; ++p)
+                    af[p] = *reinterpret_cast<const bf16x8*>(abase + p * BM * 32 + row * 32 +
+                                                             16 * (h ^ ((row >> 3) & 1)));
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    if constexpr (NP == 1) mfma_split<NP>(acc[i][j], af, bfr[j]);
+                    else drain(acc[i][j], mfma_split0<NP>(af, bfr[j]));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        // the tile's epilogue: + residual (one 16-element block's loads in flight at a time), stores
+        int64_t obase[TN];
+        bool nok[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int64_t n = n0 + wn + 32 * j + li;
+            nok[j] = n < N;
+            const int64_t nc = nok[j] ? n : N - 1;
+            const int b = (int)(nc / P);
+            obase[j] = (int64_t)b * M * P + (nc - (int64_t)b * P);
+        }
+        const bool full = m0 + BM <= M && n0 + BNT <= N;
+        if (res != nullptr) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    float q[16];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int m = min(m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
+                        q[r] = res[obase[j] + (int64_t)m * P];
+                    }
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[i][j][r] += q[r];
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+        }
+        store_tile<TM, TN>(acc, nok, obase, m0, M, P, y, full);
+    }
+}
+
 // ------------------------------------------------------------------ 3x3 weight gradient
 // dW[co][tap][ci] = sum over (b, oh, ow) of dy[b,co,oh,ow] * x[b,ci,oh+kh-1,ow+kw-1]
 // on the split path, both operands in the PSA layout with a 1-pixel border
@@ -2889,6 +3138,26 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     static const bool bn128_env = sol_env("UBPL_SOL_BN", 256) == 128;
     const bool bn128 = bn128_env && npieces == 3 && !epi && N % 128 == 0;
     const dim3 grid128((unsigned)(N / 128), (unsigned)((Cout + bm - 1) / bm));
+    // the warp-specialized persistent kernel (conv1x1_ws_kernel) for 128-row tiles whose
+    // grid fills the chip; UBPL_SOL_WS=0: conv1x1_sol_kernel
+    static const bool ws_env = sol_env("UBPL_SOL_WS", 1) != 0;
+    const int64_t ntiles = ((N + 255) / 256) * ((Cout + 127) / 128);
+    if (ws_env && bm == 128 && !epi && !bn128 && ntiles >= occ_info().ncu && (!pro || Cin <= SOL_PRO_K)) {
+        const dim3 gws((unsigned)occ_info().ncu);
+#define UBPL_WS(NP_, PRO_)                                                                                        \
+    hipLaunchKernelGGL((conv1x1_ws_kernel<NP_, PRO_>), gws, dim3(2 * NT), 0, st, x, wsplit, wplane, bias, pscale,  \
+                       pshift, res, y, B, Cin, P, Cout, (int)ntiles)
+        if (npieces == 3) {
+            if (pro) UBPL_WS(3, true);
+            else UBPL_WS(3, false);
+        } else {
+            if (pro) UBPL_WS(1, true);
+            else UBPL_WS(1, false);
+        }
+#undef UBPL_WS
+        UBPL_LAUNCH_CHECK();
+        return 0;
+    }
 #define UBPL_SOL(BM_, PRO_)                                                                                       \
     do {                                                                                                          \
         if (bn128)                                                                                                \
