@@ -260,7 +260,7 @@ int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int
  * exact-f32 ubpl_conv2d_wgrad for models/pose/hourglass.py pre.0 / layers.py:31-50):
  * dys = split(dy) (PSA, pad 1, Cout channels at the H x W output), xs = the
  * forward's phase image (ubpl_stem_s2d_split, 16 channels, pad 2); KS = 7, C <= 4
- * input channels, Cout % 64 == 0, W % 16 == 0, npieces = 3.  _workspace: slab floats. */
+ * input channels, Cout % 64 == 0, W % 16 == 0, npieces 3 or 1.  _workspace: slab floats. */
 int64_t ubpl_wgrad_stem_psa_workspace(int B, int Cout, int H, int W);
 /*@ dys:u16[(npieces-1)*dplane+(int64_t)B*Cout*(H+2)*(W+2)] xs:u16[(npieces-1)*xplane+(int64_t)B*16*(H+4)*(W+4)] slab:f32[ubpl_wgrad_stem_psa_workspace(B,Cout,H,W)] dw:f32[(int64_t)Cout*C*KS*KS] db:f32[Cout] */
 int ubpl_wgrad_stem_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int C,
@@ -288,7 +288,8 @@ int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, 
 /* The 7x7 stride-2 stem (Cin <= 4) on the split path by space-to-depth: the
  * phase images of x as a 16-channel PSA image with a `pad` (>= 2) border, and
  * the equivalent 4x4 stride-1 weights (Cin' = 16, KS' = 4) split into npieces
- * (= 3) planes of Cout*256 bf16; then ubpl_conv2d_forward_psa(..., KS = 4). */
+ * (3: 6xbf16; 1: the bf16 precision) planes of Cout*256 bf16; then
+ * ubpl_conv2d_forward_psa(..., KS = 4). */
 /*@ x:f32[(int64_t)B*C*H*W] dst:u16[(npieces-1)*plane+(int64_t)B*16*(H/2+2*pad)*(W/2+2*pad)] */
 int ubpl_stem_s2d_split(const float* x, int B, int C, int H, int W, int pad, int npieces, uint16_t* dst,
                         int64_t plane, void* stream);

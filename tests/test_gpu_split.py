@@ -591,6 +591,37 @@ def test_stem_weight_gradient_s2d_vs_f64(B, H):
         assert _rel(dw, dw32.cpu().double()) < 1e-5
 
 
+@pytest.mark.parametrize("B,H", [(2, 256), (8, 128)])
+def test_bf16_stem_s2d_forward_and_weight_gradient_vs_rounded_f64(B, H):
+    """The "bf16" precision's stem (round 5): the 7x7 stride-2 conv as the
+    space-to-depth 4x4 conv with ONE bf16 piece per operand, and its weight
+    gradient from the one-piece PSA operands — against float64 of the
+    bf16-rounded operands, to f32 summation error (the bar of the other
+    one-piece kernels)."""
+    from ubpl_amd import kernels as Kn
+    gen = torch.Generator().manual_seed(53 + B + H)
+    x = torch.rand(B, 3, H, H, generator=gen) - 0.5
+    w = torch.randn(64, 3, 7, 7, generator=gen) / np.sqrt(147)
+    b = torch.randn(64, generator=gen)
+    dy = torch.randn(B, 64, H // 2, H // 2, generator=gen)
+    bf = lambda t: t.to(torch.bfloat16).double()
+    d = lambda t: t.to(DEV)
+    yref = F.conv2d(bf(x), bf(w), b.double(), 2, 3)
+    xs = Kn.stem_s2d_split(d(x), 2, 1)
+    y = Kn.conv2d_forward_psa(xs, Kn.stem_weight_s2d_split(d(w), 1), d(b))
+    e = _rel(y, yref)
+    print("bf16 stem fwd B=%d H=%d: %.2e" % (B, H, e))
+    assert e <= 2e-6, e
+    wref = torch.nn.grad.conv2d_weight(bf(x), w.shape, bf(dy), stride=2, padding=3)
+    ys = Kn.split_activation(d(dy), 1, 1)
+    assert Kn.wgrad_stem_psa_ok(ys, xs, d(w))
+    dw, db = torch.zeros_like(d(w)), torch.zeros(64, device=DEV)
+    Kn.conv2d_wgrad_stem_psa(ys, xs, dw, db, accumulate=False)
+    e, eb = _rel(dw, wref), _rel(db, bf(dy).sum((0, 2, 3)))
+    print("bf16 stem wgrad B=%d H=%d: %.2e bias %.2e" % (B, H, e, eb))
+    assert e <= 2e-6 and eb <= 2e-6, (e, eb)
+
+
 # the halo kernel's shapes (conv_psah_kernel: 3x3 pad 1, 128- / 64-row tiles, whole
 # rows of W = 32 / 64 / 128 per 256-pixel tile): (B, Cin, H, Cout)
 HALO_CASES = [(32, 128, 64, 128), (8, 128, 128, 128), (32, 256, 32, 256), (16, 256, 64, 256),

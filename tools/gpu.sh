@@ -73,15 +73,18 @@ for step in "$@"; do
             "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 2 --warmup 1 (eager step; tools/gpu.sh pmc:bench)" psah
         rm -f $OUT/*.csv
       else
-        OUT=gpurun_out/pmc_$(basename $name .py); mkdir -p $OUT
+        # pmc:<script.py>[:ENV=V,...]: the script's environment (the program after -- stays python3)
+        OUT=gpurun_out/pmc_$(basename $name .py)${extra:+_$(echo $extra | tr ',=' '__')}; mkdir -p $OUT
         pass() {
           local n=$1; shift
-          timeout -s KILL 120 rocprofv3 --pmc "$@" -d $OUT -o $n --output-format csv -- python3 $name $(envs "$extra") > $OUT/$n.log 2>&1
+          env $(envs "$extra") timeout -s KILL 120 rocprofv3 --pmc "$@" -d $OUT -o $n --output-format csv -- python3 $name > $OUT/$n.log 2>&1
           local rc=$?; echo "pmc $n rc=$rc"; [ $rc -ne 0 ] && stop pmc $rc
         }
         pass sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT
+        pass sq2 SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE
         pass fetch FETCH_SIZE GRBM_GUI_ACTIVE
         pass write WRITE_SIZE GRBM_GUI_ACTIVE
+        rm -f $OUT/*.csv.gz 2>/dev/null; true
       fi ;;
     ab)
       IFS='|' read -ra settings <<< "$arg"

@@ -89,6 +89,9 @@ namespace {
 #ifndef UBPL_SOL_NOSPLIT
 #define UBPL_SOL_NOSPLIT 0
 #endif
+#ifndef UBPL_SOL_ACONTIG
+#define UBPL_SOL_ACONTIG 0
+#endif
 #ifndef UBPL_PSA_DMA_IL
 #define UBPL_PSA_DMA_IL 0
 #endif
@@ -1226,7 +1229,10 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     const int lr = lane >> 1;
     const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
     const bool a_issue = BM / 32 >= NT / 64 || wid < BM / 32;   // every wave when BM >= 128
-    const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, M - 1) * K + 8 * lchunk) * 2);
+    // (UBPL_SOL_ACONTIG, timing-only diagnostic: the weight DMA reads one contiguous KB per
+    // instruction instead of 32 rows' 32 B — wrong results)
+    const uint32_t a_lane = UBPL_SOL_ACONTIG ? (uint32_t)((32 * wid + lr) * 32 + 16 * lchunk)
+                                             : (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, M - 1) * K + 8 * lchunk) * 2);
     // B DMA: wave w moves k rows 4w..4w+3; 256-pixel tiles: one row per instruction,
     // lane L pixels n0 + 4L .. +3; 128-pixel tiles: two rows per instruction, lanes
     // 32-63 the second (P % 4 == 0)
@@ -1683,29 +1689,61 @@ __global__ void __launch_bounds__(2 * NT, 1) conv1x1_ws_kernel(const float* __re
             asm volatile("" ::: "memory");
             const char* abase = lds + (s % NSA) * AB;
             const char* pbase = lds + OFF_P + (s % NSP) * PB;
-            bf16x8 bfr[TN][NP];
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
+            auto read_b = [&](int j, bf16x8 (&bf)[NP]) {
                 const int px = wn + 32 * j + li;
 #pragma unroll
                 for (int p = 0; p < NP; ++p)
-                    bfr[j][p] = *reinterpret_cast<const bf16x8*>(pbase + p * (BNT * 32) + px * 32 +
-                                                                  16 * (h ^ ((px >> 3) & 1)));
-            }
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
+                    bf[p] = *reinterpret_cast<const bf16x8*>(pbase + p * (BNT * 32) + px * 32 +
+                                                             16 * (h ^ ((px >> 3) & 1)));
+            };
+            auto read_a = [&](int i, bf16x8 (&af)[NP]) {
                 const int row = 32 * i + li;
-                bf16x8 af[NP];
 #pragma unroll
                 for (int p = 0; p < NP; ++p)
                     af[p] = *reinterpret_cast<const bf16x8*>(abase + p * BM * 32 + row * 32 +
                                                              16 * (h ^ ((row >> 3) & 1)));
+            };
+            if constexpr (NP == 1) {
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
-                    if constexpr (NP == 1) mfma_split<NP>(acc[i][j], af, bfr[j]);
-                    else drain(acc[i][j], mfma_split0<NP>(af, bfr[j]));
+                    bf16x8 bf[NP];
+                    read_b(j, bf);
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) {
+                        bf16x8 af[NP];
+                        read_a(i, af);
+                        mfma_split<NP>(acc[i][j], af, bf);
+                    }
                 }
-                __builtin_amdgcn_sched_barrier(0);
+            } else {
+                // ping-pong chunks (conv_psa_kernel): tile q's 6-MFMA chain issued with tile q-1's
+                // drain adds in its gaps (the one MFMA wave per SIMD has no partner wave to cover a
+                // chain's result latency); pixel blocks outer, the A fragments re-read per tile
+                // (register budget: one B block and one A block live)
+                floatx16 prev;
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    bf16x8 bf[NP];
+                    read_b(j, bf);
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) {
+                        bf16x8 af[NP];
+                        read_a(i, af);
+                        const floatx16 cur = mfma_split0<NP>(af, bf);
+                        if (i + j > 0) {
+                            const int q = j * TM + i - 1;
+                            drain(acc[q % TM][q / TM], prev);
+#pragma unroll
+                            for (int g = 0; g < 6; ++g) {
+                                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                            }
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                        prev = cur;
+                    }
+                }
+                drain(acc[TM - 1][TN - 1], prev);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
@@ -2134,7 +2172,6 @@ __global__ void __launch_bounds__(NT, 2) wgrad_stem_psa_kernel(const uint16_t* _
     const int Go = Cout >> 4;
     constexpr int Ntot = 256, Nt = Ntot + 1;
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    static_assert(NP == 3, "6xbf16 operands");
     // grid (Cout / 64, splits): the row blocks of one split side by side (same L2)
     const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int by = lam % gridDim.x, bz = lam / gridDim.x;
@@ -2234,8 +2271,11 @@ __global__ void __launch_bounds__(NT, 2) wgrad_stem_psa_kernel(const uint16_t* _
     for (int t = 0; t < nkt; ++t) {
         // stage t landed (this wave's stage t+1 DMA may stay in flight)
         if (t + 1 < nkt) {
-            if (mine == 4) vm_wait<4>();   // (NP = 3: 15 instructions per stage, 4 / 4 / 4 / 3 per wave)
-            else vm_wait<3>();
+            // NP = 3: 15 instructions per stage (4 / 4 / 4 / 3 per wave); NP = 1: 5 (2 / 1 / 1 / 1)
+            if (mine == 4) vm_wait<4>();
+            else if (mine == 3) vm_wait<3>();
+            else if (mine == 2) vm_wait<2>();
+            else vm_wait<1>();
         } else {
             vm_wait<0>();
         }
@@ -2895,7 +2935,11 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         return !(e && atoi(e) == 0);
     }();
     if (KS == 4) {   // the space-to-depth stem (ubpl_stem_s2d_split): 64-row tiles on 256 pixels
-        if (pl.bm != 64 || pl.splits != 1 || npieces != 3 || N % 256 != 0) return (int)hipErrorInvalidValue;
+        if (pl.bm != 64 || pl.splits != 1 || (npieces != 3 && npieces != 1) || N % 256 != 0)
+            return (int)hipErrorInvalidValue;
+        if (npieces == 1)
+            return launch_psa<64, 4, 1, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout,
+                                                pl, slab, stat_part, bwd, st);
         return launch_psa<64, 4, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                             slab, stat_part, bwd, st);
     }
@@ -3140,7 +3184,7 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     const dim3 grid128((unsigned)(N / 128), (unsigned)((Cout + bm - 1) / bm));
     // the warp-specialized persistent kernel (conv1x1_ws_kernel) for 128-row tiles whose
     // grid fills the chip; UBPL_SOL_WS=0: conv1x1_sol_kernel
-    static const bool ws_env = sol_env("UBPL_SOL_WS", 1) != 0;
+    static const bool ws_env = sol_env("UBPL_SOL_WS", 0) != 0;
     const int64_t ntiles = ((N + 255) / 256) * ((Cout + 127) / 128);
     if (ws_env && bm == 128 && !epi && !bn128 && ntiles >= occ_info().ncu && (!pro || Cin <= SOL_PRO_K)) {
         const dim3 gws((unsigned)occ_info().ncu);
@@ -3274,15 +3318,20 @@ UBPL_API int ubpl_wgrad_stem_psa(const uint16_t* dys, int64_t dplane, const uint
                                  int C, int Cout, int H, int W, int KS, float* slab, float* dw, float* db,
                                  int accumulate, int npieces, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    if (npieces != 3 || KS != 7 || C < 1 || C > 4 || Cout % 64 || W % 16 || H < 1 || B < 1 || slab == nullptr)
+    if ((npieces != 3 && npieces != 1) || KS != 7 || C < 1 || C > 4 || Cout % 64 || W % 16 || H < 1 || B < 1 ||
+        slab == nullptr)
         return (int)hipErrorInvalidValue;
     if ((((uintptr_t)dys) & 15) || (((uintptr_t)xs) & 15) || (dplane % 8) || (xplane % 8))
         return (int)hipErrorInvalidValue;
     const int splits = wgrad_stem_splits(B, Cout, H, W);
     const int steps = B * H * (W / 16);
     const int per = (steps + splits - 1) / splits;
-    hipLaunchKernelGGL((wgrad_stem_psa_kernel<3>), dim3((unsigned)(Cout / 64), (unsigned)splits), dim3(NT), 0, st,
-                       dys, dplane, xs, xplane, B, Cout, H, W, per, slab);
+    if (npieces == 1)
+        hipLaunchKernelGGL((wgrad_stem_psa_kernel<1>), dim3((unsigned)(Cout / 64), (unsigned)splits), dim3(NT), 0,
+                           st, dys, dplane, xs, xplane, B, Cout, H, W, per, slab);
+    else
+        hipLaunchKernelGGL((wgrad_stem_psa_kernel<3>), dim3((unsigned)(Cout / 64), (unsigned)splits), dim3(NT), 0,
+                           st, dys, dplane, xs, xplane, B, Cout, H, W, per, slab);
     UBPL_LAUNCH_CHECK();
     float* dws = slab + (int64_t)splits * Cout * 257;
     const int e = ubpl_wgrad_slab_reduce(slab, splits, Cout, 16, 16, 1, dws, dws + (int64_t)Cout * 256, 0, stream);
@@ -3366,11 +3415,16 @@ UBPL_API int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, in
 // of the 4 phase images per channel; pad >= 2 for the 7x7 stem.
 UBPL_API int ubpl_stem_s2d_split(const float* x, int B, int C, int H, int W, int pad, int npieces, uint16_t* dst,
                                  int64_t plane, void* stream) {
-    if (C < 1 || C > 4 || (H & 1) || (W & 1) || npieces != 3 || pad < 0 || (plane % 8) != 0)
+    if (C < 1 || C > 4 || (H & 1) || (W & 1) || (npieces != 3 && npieces != 1) || pad < 0 || (plane % 8) != 0)
         return (int)hipErrorInvalidValue;
     const int Hp = H / 2 + 2 * pad, Wp = W / 2 + 2 * pad;
     dim3 grid((unsigned)((Hp * Wp + 255) / 256), (unsigned)B);
-    hipLaunchKernelGGL(stem_s2d_split_kernel<3>, grid, dim3(256), 0, (hipStream_t)stream, x, C, H, W, pad, dst, plane);
+    if (npieces == 1)
+        hipLaunchKernelGGL(stem_s2d_split_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, x, C, H, W, pad, dst,
+                           plane);
+    else
+        hipLaunchKernelGGL(stem_s2d_split_kernel<3>, grid, dim3(256), 0, (hipStream_t)stream, x, C, H, W, pad, dst,
+                           plane);
     UBPL_LAUNCH_CHECK();
     return 0;
 }
@@ -3381,10 +3435,15 @@ UBPL_API int ubpl_stem_s2d_split(const float* x, int B, int C, int H, int W, int
 UBPL_API int ubpl_stem_weight_s2d_split(const float* w, int Cout, int C, int KS, int npieces, uint16_t* dst,
                                         int64_t plane, void* stream) {
     const int KT = ((KS + 1) / 2 + 1) & ~1;
-    if (C < 1 || C > 4 || !(KS & 1) || npieces != 3 || KT != 4 || (plane % 8) != 0) return (int)hipErrorInvalidValue;
+    if (C < 1 || C > 4 || !(KS & 1) || (npieces != 3 && npieces != 1) || KT != 4 || (plane % 8) != 0)
+        return (int)hipErrorInvalidValue;
     const int64_t total = (int64_t)Cout * KT * KT * 16;
-    hipLaunchKernelGGL(stem_weight_s2d_split_kernel<3>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, w, Cout, C, KS, KT, dst, plane);
+    if (npieces == 1)
+        hipLaunchKernelGGL(stem_weight_s2d_split_kernel<1>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, w, Cout, C, KS, KT, dst, plane);
+    else
+        hipLaunchKernelGGL(stem_weight_s2d_split_kernel<3>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, w, Cout, C, KS, KT, dst, plane);
     UBPL_LAUNCH_CHECK();
     return 0;
 }

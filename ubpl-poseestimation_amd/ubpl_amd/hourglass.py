@@ -631,10 +631,12 @@ class _Exec:
 
     # ---- layers
     def stem(self, imgs):
-        if self.m.conv_pieces == 3 and _STEM_S2D and Kn.stem_s2d_ok(imgs):
+        if self.m.conv_pieces in (1, 3) and _STEM_S2D and Kn.stem_s2d_ok(imgs):
             # 7x7/s2 as a 4x4 stride-1 conv over the space-to-depth image, on the split path
-            ws = Kn.stem_weight_s2d_split(self.m.P("pre.0.conv.weight"))
-            xs = Kn.stem_s2d_split(imgs, 2)
+            # (6xbf16), or on bf16 operands (the "bf16" precision)
+            np_ = self.m.conv_pieces
+            ws = Kn.stem_weight_s2d_split(self.m.P("pre.0.conv.weight"), np_)
+            xs = Kn.stem_s2d_split(imgs, 2, np_)
             y0 = Kn.conv2d_forward_psa(xs, ws, self.m.P("pre.0.conv.bias"))
             if self.do_save and _STEM_WGRAD:
                 self.saved_split["pre.0.conv"] = xs      # the weight gradient's B operand
@@ -855,7 +857,7 @@ class _Exec:
         imgs, y0 = self.saved.get("pre.0")
         xs = self.saved_split.get("pre.0.conv")
         w0 = m.P("pre.0.conv.weight")
-        if xs is not None and m.conv_pieces == 3 and d.shape[1] % 64 == 0 and d.shape[3] % 16 == 0:
+        if xs is not None and m.conv_pieces in (1, 3) and d.shape[1] % 64 == 0 and d.shape[3] % 16 == 0:
             # dy of the stem only as the split operand of its weight gradient (the input
             # image takes no gradient): the space-to-depth 4x4 weight gradient, mapped to 7x7
             ys = self.bn_bwd_split("pre.0.bn", d, y0, relu=1)

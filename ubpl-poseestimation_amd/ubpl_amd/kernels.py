@@ -501,24 +501,25 @@ def stem_s2d_ok(x):
     return C <= 4 and H % 2 == 0 and W % 2 == 0 and (B * (H // 2) * (W // 2)) % 256 == 0
 
 
-def stem_s2d_split(x, pad=2):
+def stem_s2d_split(x, pad=2, npieces=3):
     """7x7/s2 stem input as the 16-channel PSA image of its 4 phase images
-    (space-to-depth; channels c*4 + 2ph + pw, the rest zero), border `pad`."""
+    (space-to-depth; channels c*4 + 2ph + pw, the rest zero), border `pad`;
+    npieces 3 (6xbf16) or 1 (bf16)."""
     B, C, H, W = x.shape
     Ho, Wo = H // 2, W // 2
     plane = B * (Ho + 2 * pad) * (Wo + 2 * pad) * 16
-    buf = torch.empty(3 * plane, device=x.device, dtype=torch.int16)
-    call("ubpl_stem_s2d_split", _p(x), B, C, H, W, int(pad), 3, _p(buf), int(plane))
-    return SplitAct(buf, plane, B, 16, Ho, Wo, pad, 3)
+    buf = torch.empty(npieces * plane, device=x.device, dtype=torch.int16)
+    call("ubpl_stem_s2d_split", _p(x), B, C, H, W, int(pad), int(npieces), _p(buf), int(plane))
+    return SplitAct(buf, plane, B, 16, Ho, Wo, pad, npieces)
 
 
-def stem_weight_s2d_split(w):
+def stem_weight_s2d_split(w, npieces=3):
     """The stem's 7x7 weights as the split 4x4 weights of its space-to-depth conv."""
     Cout, C, KS, _ = w.shape
     plane = Cout * 16 * 16
-    buf = torch.empty(3 * plane, device=w.device, dtype=torch.int16)
-    call("ubpl_stem_weight_s2d_split", _p(w.contiguous()), Cout, C, KS, 3, _p(buf), int(plane))
-    return SplitWeights(buf, plane, 0, (Cout, 16, 16), 3)
+    buf = torch.empty(npieces * plane, device=w.device, dtype=torch.int16)
+    call("ubpl_stem_weight_s2d_split", _p(w.contiguous()), Cout, C, KS, int(npieces), _p(buf), int(plane))
+    return SplitWeights(buf, plane, 0, (Cout, 16, 16), npieces)
 
 
 _NO_SOL = os.environ.get("UBPL_NO_SOL") == "1"      # diagnostic: every 1x1 on the exact-f32 kernels
@@ -574,7 +575,7 @@ def conv2d_wgrad3_psa(ys, xs, dw, db, accumulate=True):
 
 def wgrad_stem_psa_ok(ys, xs, w):
     Cout, C, KS = w.shape[0], w.shape[1], w.shape[2]
-    return (ys.npieces == 3 and xs.npieces == 3 and ys.pad == 1 and xs.pad == 2 and xs.C == 16 and KS == 7
+    return (ys.npieces in (1, 3) and xs.npieces == ys.npieces and ys.pad == 1 and xs.pad == 2 and xs.C == 16 and KS == 7
             and C <= 4 and Cout % 64 == 0 and ys.C == Cout and ys.W % 16 == 0
             and (ys.B, ys.H, ys.W) == (xs.B, xs.H, xs.W))
 
@@ -586,7 +587,7 @@ def conv2d_wgrad_stem_psa(ys, xs, dw, db, accumulate=True):
     n = _lib.lib().ubpl_wgrad_stem_psa_workspace(ys.B, Cout, ys.H, ys.W)
     slab = torch.empty(int(n), device=ys.buf.device, dtype=F32)
     call("ubpl_wgrad_stem_psa", _p(ys.buf), int(ys.plane), _p(xs.buf), int(xs.plane), ys.B, C, Cout, ys.H, ys.W, KS,
-         _p(slab), _p(dw), _p(db), int(accumulate), 3)
+         _p(slab), _p(dw), _p(db), int(accumulate), int(ys.npieces))
 
 
 def conv2d_dgrad(dy, w, res=None, out=None, wt=None):
