@@ -190,16 +190,17 @@ def _run_captured(cfg, monkeypatch):
     import io
     import contextlib
     import re
+    train, core = _train_fn(T, cfg)
     with contextlib.redirect_stdout(io.StringIO()):
-        T.train_mt_ubpl(list(loader) * T._StepGraph.WARM, models, emas, optims, args)
-    runner = T._StepGraph.get(T._mt_ubpl_core, models, emas, optims, args)
+        train(list(loader) * T._StepGraph.WARM, models, emas, optims, args)
+    runner = T._StepGraph.get(core, models, emas, optims, args)
     assert runner.graph is None and runner.n_eager == T._StepGraph.WARM
     torch.cuda.synchronize()
     for t, v in zip(state, snap):
         t.copy_(v)
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
-        rec = T.train_mt_ubpl(loader, models, emas, optims, args)
+        rec = train(loader, models, emas, optims, args)
     assert runner.graph is not None and runner.n_eager == T._StepGraph.WARM     # this step was the replay
     torch.cuda.synchronize()
     counts = [[int(a), int(b)] for a, b in re.findall(r"\((\s*\d+)/(\s*\d+)\)", buf.getvalue())]
@@ -209,6 +210,20 @@ def _run_captured(cfg, monkeypatch):
         full[mi] = {n: p.grad.detach().double().cpu() for n, p in m.named_parameters() if p.grad is not None}
     T._StepGraph.clear()
     return models + emas, before, rec, counts, args, grads, full
+
+
+def _train_fn(T, cfg):
+    if cfg["project"] == "DualPose_UBPL":
+        return T.train_dualpose_ubpl, T._dualpose_core
+    return T.train_mt_ubpl, T._mt_ubpl_core
+
+
+def test_captured_dualpose_step_vs_reference(monkeypatch):
+    """The DualPose_UBPL step replayed from its captured HIP graph on
+    per-network streams against the reference's fixtures (as below)."""
+    case = "dualpose"
+    cfg = seeds.step_cases()[case]
+    _check_step(case, cfg, *_run_captured(cfg, monkeypatch))
 
 
 def test_captured_b32_step_vs_reference(monkeypatch):
@@ -285,10 +300,18 @@ def test_step_graph_with_model_streams_matches_eager(monkeypatch):
     _graph_vs_eager(monkeypatch)
 
 
-def _graph_vs_eager(monkeypatch):
+def test_dualpose_step_graph_matches_eager(monkeypatch):
+    """Four DualPose_UBPL steps, captured and replayed on per-network streams,
+    bit-identical to four eager steps."""
+    monkeypatch.setenv("UBPL_MODEL_STREAMS", "1")
+    _graph_vs_eager(monkeypatch, "dualpose")
+
+
+def _graph_vs_eager(monkeypatch, case="mt_ubpl"):
     from ubpl_amd import train as T
     from ubpl_amd.optim import FlatAdamW
-    cfg = seeds.step_cases()["mt_ubpl"]
+    cfg = seeds.step_cases()[case]
+    train, core = _train_fn(T, cfg)
 
     def run(graph):
         monkeypatch.setenv("UBPL_STEP_GRAPH", "1" if graph else "0")
@@ -298,8 +321,8 @@ def _graph_vs_eager(monkeypatch):
         import io
         import contextlib
         with contextlib.redirect_stdout(io.StringIO()):
-            rec = T.train_mt_ubpl(list(loader) * 4, models, emas, optims, args)
-        runner = T._StepGraph.get(T._mt_ubpl_core, models, emas, optims, args)
+            rec = train(list(loader) * 4, models, emas, optims, args)
+        runner = T._StepGraph.get(core, models, emas, optims, args)
         assert (runner.graph is not None) == graph
         torch.cuda.synchronize()
         return [m.flat_params.clone() for m in models + emas], [m.flat_stats.clone() for m in models + emas], rec

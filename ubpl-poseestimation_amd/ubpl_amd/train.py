@@ -334,19 +334,13 @@ def _join_merge(mstreams, models):
         m.merge_alt_grads()
 
 
-def _join_and_allreduce(mstreams, models):
-    """_join_merge, then the SUM all-reduce of the students' gradients (-> DDP)."""
-    _join_merge(mstreams, models)
-    D.allreduce_grads(models)
-
-
 # ---------------------------------------------------------------------------
 # collectives of a step generator
 # ---------------------------------------------------------------------------
-# The MT_UBPL step (_mt_ubpl_core) is a generator: it YIELDS its two exchanges —
+# The MT_UBPL and DualPose steps (_mt_ubpl_core, _dualpose_core) are generators: it YIELDS its two exchanges —
 # ("sum", t): SUM all-reduce of the packed loss sums and counts in place (dist.py
 # exchange 1), ("grads", models): the students' gradient all-reduce (exchange 2)
-# — and whoever drives it performs them.  Eagerly they run at once (_drive); the
+# — and whoever drives them performs them.  Eagerly they run at once (_drive); the
 # captured step under torch.distributed captures the device work between them as
 # graph segments and runs the collectives between the segments' replays
 # (_StepGraph), so the exchanges are never inside a captured graph.
@@ -887,8 +881,99 @@ def _fdl_rows(sw, args):
 # ---------------------------------------------------------------------------
 # DualPose_UBPL
 # ---------------------------------------------------------------------------
+def _dualpose_core(models, models_ema, optims, args, stu_imgMap, stu_heatmap, ema_imgMap, meta):
+    """One DualPose_UBPL step (projects/DualPose_UBPL.py:170-290) on the device
+    with no host synchronisation, as a generator like _mt_ubpl_core: it yields
+    its two exchanges under torch.distributed and returns the packed records
+    [3M+1 losses | counts | consistency scores | pseudo scores] and the
+    host-side constants that unpack them."""
+    M = len(models)
+    dev = models[0].flat_params.device
+    S = args.nStack
+    for o in optims:
+        o.zero_grad()
+    si = stu_imgMap.to(dev, non_blocking=True).float().contiguous()
+    ei = ema_imgMap.to(dev, non_blocking=True).float().contiguous()
+    if stu_heatmap is None:
+        hm, kk = render_batch(meta["kps"].to(dev).float(), (si.shape[-2], si.shape[-1]), si.shape[-1],
+                              si.shape[-1] // 4)
+        gate = kk[:, :, 2].contiguous()
+    else:
+        hm = stu_heatmap.to(dev, non_blocking=True).float().contiguous()
+        gate = meta["kpsWeight"].to(dev, non_blocking=True).float().contiguous()
+    isl = _islabeled(meta["islabeled"], dev)
+    sw = _w(isl, 1.0, 0.0)
+    nega = _w(isl, 0.0, args.pseudoWeight)
+    cons = _w(isl, 1.0, args.pseudoWeight)
+    outs, feats, ema_l = [], [], []
+    mstreams = _ModelStreams.make(M, dev)                    # one HIP stream per network
+    for mi in range(M):                                       # :185-196
+        with (mstreams.on(mi) if mstreams else contextlib.nullcontext()):
+            o, f = models[mi](si)
+        outs.append(o)
+        feats.append(f)
+        with (mstreams.on_teacher(mi) if mstreams else contextlib.nullcontext()), torch.no_grad():
+            ema_l.append(models_ema[mi](ei)[0])
+    if mstreams:
+        mstreams.join(outs + feats + ema_l)
+        outs = [_OnMain.apply(t) for t in outs]
+        feats = [None if t is None else _OnMain.apply(t) for t in feats]
+    outs_ema = torch.stack(ema_l)
+    use_ep = getattr(args, "useEnsemblePseudo", True)    # :224 (False: epc = 0, no print)
+    K = outs[0].shape[2]
+    zero = torch.zeros((), device=dev)
+    loc, cn, cons_sc, ps_sc = [], [], [], []
+    for mi in range(M):
+        s_c, c_c, sc_c = _dist_mt2_last(outs[mi], outs_ema[mi], cons, args.pseudoScoreThr)
+        s_p, c_p = _mse(outs[mi], hm, S, gate, sw.reshape(-1, 1))
+        if use_ep:
+            s_e, c_e, sc_e = _pseudo(outs[mi], outs_ema, nega, S, args.pseudoScoreThr)
+            ps_sc.append(sc_e)
+        else:
+            s_e, c_e = zero, torch.zeros(4, dtype=torch.int32, device=dev)
+        loc += [s_c, s_p, s_e]
+        cn += [c_c[0], c_p[0], c_e[1], c_c[1], c_c[2], c_e[2]]
+        cons_sc.append(sc_c)
+    fd = []
+    if args.FDLWeight > 0:                                     # :246-270 (one view)
+        fd.append(_fdl_view(feats[0], feats[1], _fdl_rows(sw, args), args))
+    loc += _fdl_record_sums(fd)
+    cn += [n[0] for _, _, n in fd]
+    counts = torch.stack([c.float() for c in cn])
+    local = torch.stack([l.float() for l in loc])
+    if D.is_dist():
+        pack = torch.cat([counts, local.detach()])
+        yield ("sum", pack)                                  # exchange 1: global sums / counts
+        gcounts, gsums = pack[:counts.numel()], pack[counts.numel():]
+    else:
+        gcounts, gsums = _sync_stats(local, counts)
+    W = D.world()
+    fdc = _fdl_total(fd, gcounts[6 * M:], W, args.FDLWeight) if fd else 0.
+    totals = []
+    for mi in range(M):
+        mtc = args.consWeight * _norm(loc[3 * mi], gcounts[6 * mi])
+        pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[6 * mi + 1])
+        epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else 0.
+        totals.append(pec + mtc + epc + fdc)
+    _backward_all(totals, outs + feats if mstreams else None, mstreams)   # DualPose_UBPL.py:277-279
+    _join_merge(mstreams, models)
+    if D.is_dist():
+        yield ("grads", models)                              # exchange 2: SUM of the students' gradients
+    _step_and_ema(models, models_ema, optims, args)
+    g_rec = []
+    for mi in range(M):
+        g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[6 * mi + 1]),
+                  args.consWeight * _norm(gsums[3 * mi], gcounts[6 * mi]),
+                  args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else zero]
+    g_rec.append(_fdl_record(fd, gsums[3 * M:], gcounts[6 * M:], W, args.FDLWeight) if fd else zero)
+    packed = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, torch.stack(cons_sc).mean(0),
+                        torch.stack(ps_sc).mean(0) if use_ep else torch.zeros(K, device=dev)])
+    return packed, (len(cn), K, use_ep, len(fd))
+
+
 def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=True):
-    """projects/DualPose_UBPL.py:156-295."""
+    """projects/DualPose_UBPL.py:156-295.  Like train_mt_ubpl, steps after the
+    first two replay a captured HIP graph when the batch shapes repeat."""
     M = len(models)
     pec_c = [AvgCounter() for _ in range(M)]
     mtc_c = [AvgCounter() for _ in range(M)]
@@ -900,83 +985,13 @@ def train_dualpose_ubpl(trainLoader, models, models_ema, optims, args, verbose=T
         m.train()
     for e in models_ema:
         e.train()
+    runner = _StepGraph.get(_dualpose_core, models, models_ema, optims, args)
     lag = _LaggedRecords()
     with lag.flushing():
         for bat, (stu_imgMap, stu_heatmap, ema_imgMap, meta) in enumerate(trainLoader):
-            for o in optims:
-                o.zero_grad()
-            si = stu_imgMap.to(dev, non_blocking=True).float().contiguous()
-            ei = ema_imgMap.to(dev, non_blocking=True).float().contiguous()
-            if stu_heatmap is None:
-                hm, kk = render_batch(meta["kps"].to(dev).float(), (si.shape[-2], si.shape[-1]), si.shape[-1],
-                                      si.shape[-1] // 4)
-                gate = kk[:, :, 2].contiguous()
-            else:
-                hm = stu_heatmap.to(dev, non_blocking=True).float().contiguous()
-                gate = meta["kpsWeight"].to(dev, non_blocking=True).float().contiguous()
-            isl = _islabeled(meta["islabeled"], dev)
-            sw = _w(isl, 1.0, 0.0)
-            nega = _w(isl, 0.0, args.pseudoWeight)
-            cons = _w(isl, 1.0, args.pseudoWeight)
-            B = si.shape[0]
-            outs, feats, ema_l = [], [], []
-            mstreams = _ModelStreams.make(M, dev)                    # one HIP stream per network
-            for mi in range(M):                                       # :185-196
-                with (mstreams.on(mi) if mstreams else contextlib.nullcontext()):
-                    o, f = models[mi](si)
-                outs.append(o)
-                feats.append(f)
-                with (mstreams.on_teacher(mi) if mstreams else contextlib.nullcontext()), torch.no_grad():
-                    ema_l.append(models_ema[mi](ei)[0])
-            if mstreams:
-                mstreams.join(outs + feats + ema_l)
-                outs = [_OnMain.apply(t) for t in outs]
-                feats = [None if t is None else _OnMain.apply(t) for t in feats]
-            outs_ema = torch.stack(ema_l)
-            use_ep = getattr(args, "useEnsemblePseudo", True)    # :224 (False: epc = 0, no print)
-            K = outs[0].shape[2]
-            zero = torch.zeros((), device=dev)
-            loc, cn, cons_sc, ps_sc = [], [], [], []
-            for mi in range(M):
-                s_c, c_c, sc_c = _dist_mt2_last(outs[mi], outs_ema[mi], cons, args.pseudoScoreThr)
-                s_p, c_p = _mse(outs[mi], hm, S, gate, sw.reshape(-1, 1))
-                if use_ep:
-                    s_e, c_e, sc_e = _pseudo(outs[mi], outs_ema, nega, S, args.pseudoScoreThr)
-                    ps_sc.append(sc_e)
-                else:
-                    s_e, c_e = zero, torch.zeros(4, dtype=torch.int32, device=dev)
-                loc += [s_c, s_p, s_e]
-                cn += [c_c[0], c_p[0], c_e[1], c_c[1], c_c[2], c_e[2]]
-                cons_sc.append(sc_c)
-            fd = []
-            if args.FDLWeight > 0:                                     # :246-270 (one view)
-                fd.append(_fdl_view(feats[0], feats[1], _fdl_rows(sw, args), args))
-            loc += _fdl_record_sums(fd)
-            cn += [n[0] for _, _, n in fd]
-            counts = torch.stack([c.float() for c in cn])
-            gcounts, gsums = _sync_stats(torch.stack([l.float() for l in loc]), counts)
-            W = D.world()
-            fdc = _fdl_total(fd, gcounts[6 * M:], W, args.FDLWeight) if fd else 0.
-            totals = []
-            for mi in range(M):
-                mtc = args.consWeight * _norm(loc[3 * mi], gcounts[6 * mi])
-                pec = args.poseWeight * _norm(loc[3 * mi + 1], gcounts[6 * mi + 1])
-                epc = args.ensemblePseudoWeight * _norm(loc[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else 0.
-                totals.append(pec + mtc + epc + fdc)
-            _backward_all(totals, outs + feats if mstreams else None, mstreams)   # DualPose_UBPL.py:277-279
-            _join_and_allreduce(mstreams, models)
-            _step_and_ema(models, models_ema, optims, args)
-            g_rec = []
-            for mi in range(M):
-                g_rec += [args.poseWeight * _norm(gsums[3 * mi + 1], gcounts[6 * mi + 1]),
-                          args.consWeight * _norm(gsums[3 * mi], gcounts[6 * mi]),
-                          args.ensemblePseudoWeight * _norm(gsums[3 * mi + 2], gcounts[6 * mi + 2]) if use_ep else zero]
-            g_rec.append(_fdl_record(fd, gsums[3 * M:], gcounts[6 * M:], W, args.FDLWeight) if fd else zero)
-            packed = torch.cat([torch.stack([r.float() for r in g_rec]), gcounts, torch.stack(cons_sc).mean(0),
-                                torch.stack(ps_sc).mean(0) if use_ep else torch.zeros(K, device=dev)])
-            lag.push(packed, lambda host, bat=bat, ncn=len(cn), K=K, use_ep=use_ep, nfd=len(fd): _dualpose_records(
+            packed, (ncn, K, use_ep, nfd) = runner.run((stu_imgMap, stu_heatmap, ema_imgMap, meta), dev)
+            lag.push(packed, lambda host, bat=bat, ncn=ncn, K=K, use_ep=use_ep, nfd=nfd: _dualpose_records(
                 host, bat, ncn, K, use_ep, nfd, M, S, pec_c, mtc_c, epc_c, fdc_c, args, verbose))
-            del outs, outs_ema, feats, totals
     return ([c.avg for c in pec_c], [c.avg for c in mtc_c], [c.avg for c in epc_c], fdc_c.avg)
 
 
