@@ -44,13 +44,13 @@ for step in "$@"; do
       if [ $rc -ne 0 ]; then grep -E "^(FAILED|ERROR)|Error|assert" gpurun_out/pytest.log | head -20; stop tests $rc; fi ;;
     bench)
       c=$(cfg $name); [ $name = eager ] && extra="UBPL_STEP_GRAPH=0${extra:+,$extra}"
-      tag=$name${extra:+_$(echo $extra | tr ',=' '__')}
+      tag=$name${extra:+_$(echo $extra | tr ',=/' '___')}
       env $(envs "$extra") timeout -k 10 ${BENCH_TIMEOUT:-500} python bench.py --config $c --steps ${STEPS:-20} \
           --warmup ${WARM:-3} $([ "$CPU" = 1 ] || echo --no-cpu-baseline) > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err
       rc=$?; [ $rc -ne 0 ] && { tail -5 gpurun_out/bench_$tag.err; stop bench $rc; }
       python -c "import json;d=json.load(open('gpurun_out/bench_$tag.json'));r=d['roofline'] or {};print('bench $tag:', d['value'], 'img/s', d['ms_per_step'], 'ms; roofline', r.get('avg_launch_us'), 'us frac', r.get('frac'), '; cpu', (d['cpu_baseline'] or {}).get('value'))" ;;
     prof)
-      c=$(cfg $name); tag=$name${extra:+_$(echo $extra | tr ',=' '__')}
+      c=$(cfg $name); tag=$name${extra:+_$(echo $extra | tr ',=/' '___')}
       rm -rf gpurun_out/prof_$tag; mkdir -p gpurun_out/prof_$tag
       env $(envs "$extra") timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run \
           --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 2 --no-cpu-baseline \
@@ -74,7 +74,7 @@ for step in "$@"; do
         rm -f $OUT/*.csv
       else
         # pmc:<script.py>[:ENV=V,...]: the script's environment (the program after -- stays python3)
-        OUT=gpurun_out/pmc_$(basename $name .py)${extra:+_$(echo $extra | tr ',=' '__')}; mkdir -p $OUT
+        OUT=gpurun_out/pmc_$(basename $name .py)${extra:+_$(echo $extra | tr ',=/' '___')}; mkdir -p $OUT
         pass() {
           local n=$1; shift
           env $(envs "$extra") timeout -s KILL 120 rocprofv3 --pmc "$@" -d $OUT -o $n --output-format csv -- python3 $name > $OUT/$n.log 2>&1

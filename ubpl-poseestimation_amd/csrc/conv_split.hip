@@ -104,6 +104,14 @@ namespace {
 #ifndef UBPL_SOL_LDS_COEF
 #define UBPL_SOL_LDS_COEF 1
 #endif
+// timing-only: conv1x1_sol_kernel's DMA ring, waits and barriers without the compute
+#ifndef UBPL_SOL_NOCOMP
+#define UBPL_SOL_NOCOMP 0
+#endif
+// timing-only: conv1x1_sol_kernel's compute on stale LDS, no DMA
+#ifndef UBPL_SOL_NODMA
+#define UBPL_SOL_NODMA 0
+#endif
 
 constexpr int NT = 256;
 constexpr bool PSA_WS = false;   // conv_psa_kernel 128 x 256 tiles, 6xbf16: warp-specialized variant (opt-in, measured no gain: DESIGN §6)
@@ -1246,7 +1254,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     }
     auto stage_a = [&](int buf, int kt) {
         char* base = lds + buf * AB;
-        if (a_issue) {
+        if (a_issue && !UBPL_SOL_NODMA) {
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
                 const char* ab = reinterpret_cast<const char*>(wp + p * wplane + kt);
@@ -1257,6 +1265,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     };
     auto stage_b = [&](int buf, int kt) {
         char* base = lds + NS * AB + buf * BB;
+        if (UBPL_SOL_NODMA) return;
 #pragma unroll
         for (int q = 0; q < BQ; ++q) {
             const int r = 4 * wid + q * (4 / BQ);
@@ -1301,6 +1310,52 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
 
     const int nkt = K >> 4;
     constexpr bool deepb = NSB != NS;
+    // this lane's k half of K step kt: 8 (scale, shift) pairs of the prologue
+    auto load_coef = [&](int kt, float (&sc)[8], float (&sh)[8]) {
+        if (PRO && !UBPL_SOL_LDS_COEF) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float s0 = pscale[kt + e], s1 = pscale[kt + 8 + e];
+                const float h0 = pshift[kt + e], h1 = pshift[kt + 8 + e];
+                sc[e] = h ? s1 : s0;
+                sh[e] = h ? h1 : h0;
+            }
+        } else if (PRO) {
+            const float4* qs = reinterpret_cast<const float4*>(lds_sc + kt + 8 * h);
+            const float4* qh = reinterpret_cast<const float4*>(lds_sh + kt + 8 * h);
+            const float4 s0 = qs[0], s1 = qs[1], h0 = qh[0], h1 = qh[1];
+            sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+            sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+            sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
+            sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+        }
+    };
+    // this wave's B fragment of pixel column j (32 pixels) from a B stage: 8 f32 per lane,
+    // prologue, split into NP bf16 pieces
+    auto split_col = [&](const char* bbase, int j, const float (&sc)[8], const float (&sh)[8], bf16x8 (&out)[NP]) {
+        const float* bs = reinterpret_cast<const float*>(bbase + h * BH) + wn + li;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            v[e] = bs[e * BNT + 32 * j];
+            if (PRO) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
+        }
+        uint32_t pk[NP][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            uint32_t o[NP];
+            if (UBPL_SOL_NOSPLIT) split2<1>(v[2 * e], v[2 * e + 1], *reinterpret_cast<uint32_t(*)[1]>(o));
+            if (UBPL_SOL_NOSPLIT) for (int p = 1; p < NP; ++p) o[p] = o[0] ^ (uint32_t)p;
+            else split2<NP>(v[2 * e], v[2 * e + 1], o);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) pk[p][e] = o[p];
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            const uint4 u = make_uint4(pk[p][0], pk[p][1], pk[p][2], pk[p][3]);
+            out[p] = __builtin_bit_cast(bf16x8, u);
+        }
+    };
     stage(0, 0);
     if (NS == 3 && nkt > 1) stage(1, 16);
     if (deepb && nkt > 1) stage_b(1, 16);
@@ -1325,54 +1380,15 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         } else if (t + NS - 1 < nkt) {
             stage((t + NS - 1) % NS, (t + NS - 1) * 16);
         }
+        if (UBPL_SOL_NOCOMP) continue;
         const int kt = t * 16;
         const char* base = lds + (t % NS) * AB;                       // A of stage t
         const char* bbase = lds + NS * AB + (t % NSB) * BB;           // B of stage t
-        // this lane's k half: 8 (scale, shift) pairs
         float sc[8], sh[8];
-        if (PRO && !UBPL_SOL_LDS_COEF) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float s0 = pscale[kt + e], s1 = pscale[kt + 8 + e];
-                const float h0 = pshift[kt + e], h1 = pshift[kt + 8 + e];
-                sc[e] = h ? s1 : s0;
-                sh[e] = h ? h1 : h0;
-            }
-        } else if (PRO) {
-            const float4* qs = reinterpret_cast<const float4*>(lds_sc + kt + 8 * h);
-            const float4* qh = reinterpret_cast<const float4*>(lds_sh + kt + 8 * h);
-            const float4 s0 = qs[0], s1 = qs[1], h0 = qh[0], h1 = qh[1];
-            sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
-            sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
-            sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
-            sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
-        }
-        const float* bs = reinterpret_cast<const float*>(bbase + h * BH) + wn + li;
+        load_coef(kt, sc, sh);
         bf16x8 bfr[TN][NP];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                v[e] = bs[e * BNT + 32 * j];
-                if (PRO) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
-            }
-            uint32_t pk[NP][4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                uint32_t o[NP];
-                if (UBPL_SOL_NOSPLIT) split2<1>(v[2 * e], v[2 * e + 1], *reinterpret_cast<uint32_t(*)[1]>(o));
-                if (UBPL_SOL_NOSPLIT) for (int p = 1; p < NP; ++p) o[p] = o[0] ^ (uint32_t)p;
-                else split2<NP>(v[2 * e], v[2 * e + 1], o);
-#pragma unroll
-                for (int p = 0; p < NP; ++p) pk[p][e] = o[p];
-            }
-#pragma unroll
-            for (int p = 0; p < NP; ++p) {
-                const uint4 u = make_uint4(pk[p][0], pk[p][1], pk[p][2], pk[p][3]);
-                bfr[j][p] = __builtin_bit_cast(bf16x8, u);
-            }
-        }
+        for (int j = 0; j < TN; ++j) split_col(bbase, j, sc, sh, bfr[j]);
         if constexpr (NP == 1) {
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
