@@ -104,13 +104,46 @@ namespace {
 #ifndef UBPL_SOL_LDS_COEF
 #define UBPL_SOL_LDS_COEF 1
 #endif
+// conv1x1_sol_kernel's A (weight) fragment reads: 0 each row block's at its head, 1 the
+// same without the scheduling barrier between row blocks, 2 one row block ahead
+#ifndef UBPL_SOL_APF
+#define UBPL_SOL_APF 0
+#endif
 // timing-only: conv1x1_sol_kernel's DMA ring, waits and barriers without the compute
 #ifndef UBPL_SOL_NOCOMP
 #define UBPL_SOL_NOCOMP 0
 #endif
-// timing-only: conv1x1_sol_kernel's compute on stale LDS, no DMA
+// timing-only: conv1x1_sol_kernel's compute on stale LDS, no DMA; 1: none, 2: no weight
+// DMA (activations only), 3: half the activation rows' DMA (weights all)
 #ifndef UBPL_SOL_NODMA
 #define UBPL_SOL_NODMA 0
+#endif
+
+// diagnostic build only (UBPL_CLOCK_STAMP=1): conv_psah_kernel and conv1x1_sol_kernel record
+// per workgroup the shader-clock and the 100 MHz real-time counter deltas from entry to the
+// epilogue (lane 0 of wave 0, plain vector stores into a buffer of their own); the in-kernel
+// clock is their ratio x 100 MHz (ubpl_debug_clock_stamps, tools/clock_probe.py)
+#ifndef UBPL_CLOCK_STAMP
+#define UBPL_CLOCK_STAMP 0
+#endif
+#if UBPL_CLOCK_STAMP
+__device__ unsigned long long g_clk_stamp[2][1 << 16];
+#define UBPL_STAMP_BEGIN                                                   \
+    const unsigned long long stamp_t0 = __builtin_amdgcn_s_memtime(),     \
+                             stamp_r0 = __builtin_amdgcn_s_memrealtime();
+#define UBPL_STAMP_END                                                                      \
+    {                                                                                       \
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(),                        \
+                                 r1 = __builtin_amdgcn_s_memrealtime();                    \
+        if (threadIdx.x == 0) {                                                             \
+            const int sb = (blockIdx.x + gridDim.x * blockIdx.y) & 0xffff;                  \
+            g_clk_stamp[0][sb] = t1 - stamp_t0;                                             \
+            g_clk_stamp[1][sb] = r1 - stamp_r0;                                             \
+        }                                                                                   \
+    }
+#else
+#define UBPL_STAMP_BEGIN
+#define UBPL_STAMP_END
 #endif
 
 constexpr int NT = 256;
@@ -893,6 +926,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
                                                         int B, int Cin, int H, int Cout) {
+    UBPL_STAMP_BEGIN
     constexpr int BNT = BNT1 * TEAMS, R = BNT / WW, W2 = WW + 2;
     static_assert(BNT1 == 256 || (BNT1 == 192 && BM == 128), "192-pixel tiles: 128 rows");
     constexpr int NW = 4 * TEAMS;              // waves (TEAMS 4-wave teams, one 256-pixel tile each)
@@ -1166,6 +1200,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
     }
+    UBPL_STAMP_END
 
     int64_t obase[TN];
     bool nok[TN];
@@ -1202,6 +1237,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     // NS: stages in the LDS ring (2, or 3 with 64-row tiles: two K steps' DMA in flight);
     // NSB = 3 with NS = 2: a deeper ring for the activation stream alone (HBM: two K
     // steps of it in flight per workgroup) beside the weights' two stages (L2-resident)
+    UBPL_STAMP_BEGIN
     static_assert(BNT == 256 || BNT == 128, "256- or 128-pixel tiles");
     static_assert(NSB == NS || (NS == 2 && NSB == 3), "B ring: as deep as A's, or 3 beside A's 2");
     constexpr int TM = BM / 32, TN = BNT / 128;
@@ -1254,7 +1290,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     }
     auto stage_a = [&](int buf, int kt) {
         char* base = lds + buf * AB;
-        if (a_issue && !UBPL_SOL_NODMA) {
+        if (a_issue && UBPL_SOL_NODMA != 1 && UBPL_SOL_NODMA != 2) {
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
                 const char* ab = reinterpret_cast<const char*>(wp + p * wplane + kt);
@@ -1265,9 +1301,9 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     };
     auto stage_b = [&](int buf, int kt) {
         char* base = lds + NS * AB + buf * BB;
-        if (UBPL_SOL_NODMA) return;
+        if (UBPL_SOL_NODMA == 1) return;
 #pragma unroll
-        for (int q = 0; q < BQ; ++q) {
+        for (int q = 0; q < (UBPL_SOL_NODMA == 3 ? BQ / 2 : BQ); ++q) {
             const int r = 4 * wid + q * (4 / BQ);
             const char* bb = reinterpret_cast<const char*>(x + (int64_t)(kt + r) * P);
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
@@ -1399,42 +1435,61 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
                 for (int j = 0; j < TN; ++j) mfma_split<NP>(acc[i][j], af, bfr[j]);
             }
         } else {
-#if UBPL_SOL_PP
-        // ping-pong chunks (as conv_psa_kernel): tile (i, j)'s chain is issued
-        // with the previous tile's drain adds between its MFMAs
-        floatx16 prev;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
+        auto lda = [&](int i, bf16x8 (&o)[NP]) {
             const int row = 32 * i + li;
-            bf16x8 af[NP];
 #pragma unroll
             for (int p = 0; p < NP; ++p)
-                af[p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+                o[p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+        };
+#if UBPL_SOL_PP
+        // ping-pong chunks (as conv_psa_kernel): tile (i, j)'s chain is issued with the
+        // previous tile's drain adds between its MFMAs, and row block i+1's A fragments
+        // are read during row block i (one continuous MFMA stream over the K step)
+        floatx16 prev;
+        bf16x8 afc[NP], afn[NP];
+        lda(0, afc);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const floatx16 cur = mfma_split0<NP>(af, bfr[j]);
+                const floatx16 cur = mfma_split0<NP>(afc, bfr[j]);
+                const bool pf = j == 0 && i + 1 < TM;
+                if (pf) lda(i + 1, afn);
                 if (i + j > 0) {
                     const int q = i * TN + j - 1;
                     drain(acc[q / TN][q % TN], prev);
+                    // the prefetch after the chain's first MFMA: the wait the compiler puts
+                    // before that MFMA (for this row's fragments) then covers no new read
 #pragma unroll
                     for (int g = 0; g < 6; ++g) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                         __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                        if (g == 0 && pf) __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 prev = cur;
             }
+            if (i + 1 < TM) {
+#pragma unroll
+                for (int p = 0; p < NP; ++p) afc[p] = afn[p];
+            }
         }
         drain(acc[TM - 1][TN - 1], prev);
 #else
+        bf16x8 afn[NP];
+        if (UBPL_SOL_APF == 2) lda(0, afn);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-            const int row = 32 * i + li;
             bf16x8 af[NP];
+            if (UBPL_SOL_APF == 2) {
+                // row block i+1's A fragments read ahead of row block i's MFMAs
 #pragma unroll
-            for (int p = 0; p < NP; ++p)
-                af[p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
+                for (int p = 0; p < NP; ++p) af[p] = afn[p];
+                if (i + 1 < TM) lda(i + 1, afn);
+            } else {
+                lda(i, af);
+            }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 // per-chunk accumulation (see conv_fwd_split_kernel)
@@ -1442,12 +1497,13 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
                 else drain(acc[i][j], mfma_split0<NP>(af, bfr[j]));
             }
             // (register budget: one row block's A fragments live at a time)
-            __builtin_amdgcn_sched_barrier(0);
+            if (UBPL_SOL_APF != 1) __builtin_amdgcn_sched_barrier(0);
         }
 #endif
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    UBPL_STAMP_END
 
     out_base(obase, nok);
     if constexpr (EPI) {
@@ -2914,6 +2970,20 @@ PsaDispatch psa_dispatch() {
     return {g_psa_halo.load(std::memory_order_relaxed), g_psa_teams.load(std::memory_order_relaxed)};
 }
 }  // namespace
+
+#if UBPL_CLOCK_STAMP
+// (diagnostic build only; not in the header) the stamps of the last launches: n <= 65536
+// (memtime delta, realtime delta) pairs
+extern "C" __attribute__((visibility("default"))) int ubpl_debug_clock_stamps(unsigned long long* out, int n) {
+    if (n < 0 || n > (1 << 16)) return (int)hipErrorInvalidValue;
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk_stamp), sizeof(unsigned long long) * n, 0,
+                                       hipMemcpyDeviceToHost);
+    if (e == hipSuccess)
+        e = hipMemcpyFromSymbol(out + n, HIP_SYMBOL(g_clk_stamp), sizeof(unsigned long long) * n,
+                                sizeof(unsigned long long) * (1 << 16), hipMemcpyDeviceToHost);
+    return (int)e;
+}
+#endif
 
 UBPL_API int ubpl_set_psa_dispatch(int halo_mode, int teams) {
     if (halo_mode < -1 || halo_mode > 3 || teams < -1 || teams > 2) return (int)hipErrorInvalidValue;
