@@ -243,7 +243,8 @@ int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int KS, int 
 /* Test hook (host-only): the 3x3 input-halo kernel dispatch of
  * ubpl_conv2d_forward_psa.  halo_mode -1 default, 0 off, 1 on where eligible,
  * 2 on and required (an ineligible 3x3 launch returns hipErrorInvalidValue),
- * 3 the one-buffer variant required; teams -1 default, 1 / 2 teams per
+ * 3 the one-buffer variant required, 4 the one-buffer variant on 16x16x32
+ * MFMAs (paired piece products) required; teams -1 default, 1 / 2 teams per
  * workgroup.  The environment (UBPL_PSA_HALO = 0 / 1, UBPL_PSA_TEAMS) sets the
  * initial values, read once. */
 int ubpl_set_psa_dispatch(int halo_mode, int teams);

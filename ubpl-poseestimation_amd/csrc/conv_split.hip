@@ -23,6 +23,7 @@
 using ubpl::xcd_remap;
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short short8 __attribute__((ext_vector_type(8)));
@@ -921,7 +922,13 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
 // tap (a second barrier then), the partner workgroup's MFMAs covering that bubble.
 // BNT1: pixels per team tile — 256, or 192 for the 96-wide planes (two rows; 128-row
 // tiles only: wave tile 64 x 96, three 32-pixel fragments)
-template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2, int BNT1 = 256>
+// M16 (6xbf16, one halo buffer): the matrix work on v_mfma_f32_16x16x32_bf16 with the six
+// piece products paired along K — (hi.lo + lo.hi), (hi.mid + mid.hi), (mid.mid + hi.hi), the
+// A fragment [X | Y] and the B fragment [U | V] being pieces X, Y / U, V of the same 16
+// channels in the two k halves — so three 32-k MFMAs per 16 x 16 tile and K step, the same
+// MFMA cycles as six 32x32x16 per 32 x 32 tile.  The chip holds a higher clock on this shape
+// (the roofline kernel is DVFS-held: DESIGN §6 round 5); a 16 x 16 tile drains 4 adds.
+template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2, int BNT1 = 256, bool M16 = false>
 __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
@@ -958,7 +965,9 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
     constexpr int NA = GS ? 9 * NS_G : (NHB == 1 ? NA1 : 3);   // A images
     constexpr int WGM = BM / 64, WGN = 4 / WGM;
     constexpr int TM = 2, TN = BNT1 / WGN / 32;
+    constexpr int TM16 = 4, TN16 = BNT1 / WGN / 16;   // M16: 16 x 16 blocks of the 64-row wave tile
     static_assert(BM == 64 || BM == 128, "64- or 128-row tiles");
+    static_assert(!M16 || (NP == 3 && TEAMS == 1 && NHB == 1), "M16: 6xbf16, one halo buffer");
     constexpr int OFF_H = NA * AB, LDS_BYTES = OFF_H + (GS ? NS_G : NHB) * NP * HB;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS");
     static_assert(BNT % WW == 0 && WW % 32 == 0, "whole rows of 32-pixel fragments");
@@ -1008,7 +1017,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             const int i = min(wid * NH + u, HTOT - 1);  // (a spare repeats the last: same bytes)
             const int p = i / HI, c0 = min((i - p * HI) * 32, HPX - 32);
             const int q = c0 + lr;
-            const int ch = lo ^ ((q >> 3) & 1);
+            const int ch = M16 ? lo : lo ^ ((q >> 3) & 1);   // (M16: unswizzled, see step16)
             const char* src = reinterpret_cast<const char*>(xs + p * xplane + (gpx + q) * 16) + ch * 16;
             char* dst = lds + OFF_H + (buf * NP + p) * HB + c0 * 32;
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
@@ -1028,7 +1037,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             const int i = min(wid * BW + u, BT - 1);
             const int p = i / BI, c0 = R0 * W2 + min((i - p * BI) * 32, BPX - 32);
             const int q = c0 + lr;
-            const int ch = lo ^ ((q >> 3) & 1);
+            const int ch = M16 ? lo : lo ^ ((q >> 3) & 1);
             const char* src = reinterpret_cast<const char*>(xs + p * xplane + (gpx + q) * 16) + ch * 16;
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(lds + OFF_H + p * HB + c0 * 32), 16, 0, 0);
         }
@@ -1050,8 +1059,35 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
     };
     // halo pixel of tap (0, 0) for tile-local output pixel nt: row nt / WW, column nt % WW
     const int nt0 = wn + li;
-    floatx16 acc[TM][TN];
-    {
+    floatx16 acc[TM][TN];   // (dead with M16)
+    // M16: lane (c16 = lane % 16, kc = lane / 16): fragment row / column c16, k chunk kc (8
+    // channels: chunk kc & 1 of piece X (kc < 2) or Y); output rows 4 kc + r of column c16
+    const int c16 = lane & 15, kc = lane >> 4;
+    floatx4 acc4[M16 ? TM16 : 1][M16 ? TN16 : 1];
+    auto out_base16 = [&](int j, int64_t& ob, bool& ok) {
+        const int64_t n = n0 + wn + 16 * j + c16;
+        ok = n < N;
+        const int64_t nc = ok ? n : N - 1;
+        const int bb = (int)(nc / P);
+        ob = (int64_t)bb * Cout * P + (nc - (int64_t)bb * P);
+    };
+    if constexpr (M16) {
+#pragma unroll
+        for (int j = 0; j < TN16; ++j) {
+            int64_t ob;
+            bool ok;
+            out_base16(j, ob, ok);
+#pragma unroll
+            for (int i = 0; i < TM16; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = min(m0 + wm + 16 * i + 4 * kc + r, Cout - 1);
+                    float v = bias != nullptr ? bias[m] : 0.f;
+                    if (res != nullptr) v += res[ob + (int64_t)m * P];
+                    acc4[i][j][r] = v;
+                }
+        }
+    } else {
         int64_t obase[TN];
         bool nok[TN];
         out_base(obase, nok);
@@ -1060,7 +1096,83 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
 
     // one K step (group cg's tap at pixel offset toff): fragments from the A image
     // at abase and the halo image at hbase
+    // M16 K step: A fragments of the four row blocks ([hi|lo], [hi|mid], [mid|hi]); per 16-pixel
+    // block the B fragments [lo|hi], [mid|hi] (read one block ahead); per tile the chain
+    // (hi.lo + lo.hi) -> (hi.mid + mid.hi) -> (mid.mid + hi.hi) from zero, drained with 4 adds
+    // (M16) per-lane byte offsets of the B rows at tap (0, 0), one per 16-pixel block: the
+    // halo is unswizzled for this kernel (16 consecutive pixels per read group: no bank
+    // conflict), so a K step adds only its uniform tap offset
+    uint32_t boff[M16 ? TN16 : 1];
+    if constexpr (M16) {
+#pragma unroll
+        for (int j = 0; j < TN16; ++j) {
+            const int nt = wn + 16 * j + c16;
+            boff[j] = (uint32_t)((nt + (nt / WW) * 2) * 32 + 16 * (kc & 1));
+        }
+    }
+    auto step16 = [&](const char* abase, const char* hbase, int toff) {
+        const int ch = kc & 1, yh = kc >> 1;
+        bf16x8 a1[TM16], a2[TM16], a3[TM16];
+#pragma unroll
+        for (int i = 0; i < TM16; ++i) {
+            const int row = wm + 16 * i + c16;
+            const char* ar = abase + row * 32 + 16 * (ch ^ ((row >> 3) & 1));
+            a1[i] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 2 : 0) * BM * 32);
+            a2[i] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 1 : 0) * BM * 32);
+            a3[i] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 0 : 1) * BM * 32);
+        }
+        const char* hb_t = hbase + toff * 32;
+        auto read_b16 = [&](int j, bf16x8& b1, bf16x8& b2) {
+            const char* br = hb_t + boff[j];
+            b1 = *reinterpret_cast<const bf16x8*>(br + (yh ? 0 : 2) * HB);
+            b2 = *reinterpret_cast<const bf16x8*>(br + (yh ? 0 : 1) * HB);
+        };
+        bf16x8 b1, b2, n1, n2;
+        read_b16(0, b1, b2);
+        const floatx4 zero = {};
+        // ping-pong: tile q's chain issued with tile q-1's four drain adds in its gaps
+        floatx4 prev;
+#pragma unroll
+        for (int q = 0; q < TM16 * TN16; ++q) {
+            const int j = q / TM16, i = q % TM16;
+            if (i == 0 && j > 0) {
+                b1 = n1;
+                b2 = n2;
+            }
+            floatx4 cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1, zero, 0, 0, 0);
+            cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[i], b2, cur, 0, 0, 0);
+            cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[i], b2, cur, 0, 0, 0);
+            const bool pf = i == 0 && j + 1 < TN16;
+            if (pf) read_b16(j + 1, n1, n2);
+            if (q > 0) {
+                const int pj = (q - 1) / TM16, pi = (q - 1) % TM16;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = acc4[pi][pj][r] + prev[r];
+                    asm("" : "+v"(v));
+                    acc4[pi][pj][r] = v;
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                if (pf) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            prev = cur;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = acc4[TM16 - 1][TN16 - 1][r] + prev[r];
+            asm("" : "+v"(v));
+            acc4[TM16 - 1][TN16 - 1][r] = v;
+        }
+    };
     auto step = [&](const char* abase, const char* hbase, int toff) {
+        if constexpr (M16) {
+            step16(abase, hbase, toff);
+        } else {
         bf16x8 af[TM][NP], bfr[TN][NP];
         auto read_b = [&](int j) {
             const int nt = nt0 + 32 * j;
@@ -1107,6 +1219,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
                 prev = cur;
             }
             drain(acc[TM - 1][TN - 1], prev);
+        }
         }
     };
 
@@ -1202,10 +1315,31 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
     }
     UBPL_STAMP_END
 
-    int64_t obase[TN];
-    bool nok[TN];
-    out_base(obase, nok);
-    store_tile<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, y, m0 + BM <= Cout && n0 + BNT <= N);
+    if constexpr (M16) {
+#pragma unroll
+        for (int j = 0; j < TN16; ++j) {
+            int64_t ob;
+            bool ok;
+            out_base16(j, ob, ok);
+            if (!ok) continue;
+#pragma unroll
+            for (int i = 0; i < TM16; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = m0 + wm + 16 * i + 4 * kc + r;
+                    if (m < Cout) {
+                        float* d = y + ob + (int64_t)m * P;
+                        if (UBPL_NT_EPI) __builtin_nontemporal_store(acc4[i][j][r], d);
+                        else *d = acc4[i][j][r];
+                    }
+                }
+        }
+    } else {
+        int64_t obase[TN];
+        bool nok[TN];
+        out_base(obase, nok);
+        store_tile<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, y, m0 + BM <= Cout && n0 + BNT <= N);
+    }
 }
 
 // ------------------------------------------------------------------ 1x1, split on load
@@ -2986,7 +3120,7 @@ extern "C" __attribute__((visibility("default"))) int ubpl_debug_clock_stamps(un
 #endif
 
 UBPL_API int ubpl_set_psa_dispatch(int halo_mode, int teams) {
-    if (halo_mode < -1 || halo_mode > 3 || teams < -1 || teams > 2) return (int)hipErrorInvalidValue;
+    if (halo_mode < -1 || halo_mode > 4 || teams < -1 || teams > 2) return (int)hipErrorInvalidValue;
     psa_dispatch();                       // the environment's values are read first, then replaced
     g_psa_halo.store(halo_mode);
     g_psa_teams.store(teams);
@@ -3059,10 +3193,11 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     // every eligible launch on the double-buffered halo (two teams where the grid fills the
     // chip); test-only through ubpl_set_psa_dispatch: 2: as 1, required (a 3x3 launch the
     // kernel cannot take is an error); 3: the one-buffer variant for every eligible 6xbf16
-    // launch, required.  The tests compare the kernels in one process; they compute in the
-    // same order, bit for bit.
+    // launch, required; 4: as 3 on the 16x16x32 form (M16: the paired-piece products, a
+    // different summation order).  The tests compare the kernels in one process; modes 0-3
+    // compute in the same order, bit for bit.
     const int halo_mode = psa_dispatch().halo;
-    const bool one_buf = npieces == 3 && (halo_mode == 3 || halo_mode < 0);
+    const bool one_buf = npieces == 3 && (halo_mode == 3 || halo_mode == 4 || halo_mode < 0);
     // the 96-wide planes: 192-pixel tiles on 128 rows whatever the plan's row block (its
     // cost model is conv_psa_kernel's), the one-buffer variant only
     const bool w96 = W == 96 && Cout % 128 == 0 && H % 2 == 0 &&
@@ -3070,7 +3205,7 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     const bool halo_ok = KS == 3 && pad == 1 && npieces != 2 && pl.splits == 1 && !stat_part && !bwd.part &&
                          (((pl.bm == 128 || bm64w) && (W == 32 || W == 64 || W == 128) && H % (256 / W) == 0) ||
                           w96);
-    if ((halo_mode == 2 || halo_mode == 3) && KS == 3 && npieces != 2 && !halo_ok) return (int)hipErrorInvalidValue;
+    if ((halo_mode >= 2) && KS == 3 && npieces != 2 && !halo_ok) return (int)hipErrorInvalidValue;
     const bool halo = halo_mode < 0 ? ((npieces == 1 && W <= 64) || one_buf) : halo_mode != 0;
     if (halo && halo_ok) {
         // two 4-wave teams per workgroup (512 pixels: one halo, one A ring for both,
@@ -3114,9 +3249,21 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         }
         const dim3 grid((unsigned)(N / 256), (unsigned)mt);
         if (one_buf) {   // one halo buffer, two workgroups per CU
+            // the 16x16x32 form (UBPL_PSAH16=1)
+            static const bool m16_env = [] {
+                const char* e = std::getenv("UBPL_PSAH16");
+                return e != nullptr && std::atoi(e) != 0;
+            }();
+            const bool m16 = halo_mode == 4 || (halo_mode < 0 && m16_env);
 #define UBPL_PSAH1(W_, BM_)                                                                                   \
-    hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 1, 1>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane, \
-                       bias, res, y, B, Cin, H, Cout)
+    do {                                                                                                      \
+        if (m16)                                                                                              \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 1, 1, 256, true>), grid, dim3(NT), 0, st, xs,    \
+                               xplane, wsplit, wplane, bias, res, y, B, Cin, H, Cout);                        \
+        else                                                                                                  \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 1, 1>), grid, dim3(NT), 0, st, xs, xplane, wsplit, \
+                               wplane, bias, res, y, B, Cin, H, Cout);                                        \
+    } while (0)
             if (pl.bm == 128) {
                 if (W == 64) UBPL_PSAH1(64, 128);
                 else if (W == 128) UBPL_PSAH1(128, 128);
