@@ -23,6 +23,7 @@ from ubpl_amd import _lib  # noqa: E402
 from ubpl_amd import kernels as Kn  # noqa: E402
 
 SPLIT_PEAK = 2500.0 / 6          # f32-equivalent TF/s of 6 bf16 products at the dense bf16 peak
+TIMELINE = os.environ.get("UBPL_PROBE_TIMELINE") == "1"   # with a UBPL_CLOCK_STAMP=2 build
 
 
 def stamps(lib, n):
@@ -49,6 +50,23 @@ def probe(name, fn, nwg, flops, seconds, lib):
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / 20
     dt, dr = stamps(lib, nwg)
+    if TIMELINE:
+        # UBPL_CLOCK_STAMP=2 build: absolute real-time (100 MHz) at workgroup entry / exit
+        t0 = dt.min()
+        st, en = (dt - t0) / 100.0, (dr - t0) / 100.0            # us
+        print("%-34s %.3f ms/launch; last launch: span %.1f us, workgroup starts 0 .. %.1f us (median %.1f),"
+              " lifetimes median %.1f us (p10 %.1f p90 %.1f), ends median %.1f us, last %.1f us"
+              % (name, ms, en.max(), st.max(), np.median(st), np.median(en - st), np.percentile(en - st, 10),
+                 np.percentile(en - st, 90), np.median(en), en.max()))
+        # by XCD (dispatch order: linear workgroup id mod 8) and by tile (the kernels' XCD remap
+        # gives XCD x the tiles x*n/8 .. (x+1)*n/8 - 1)
+        lt = en - st
+        ids = np.arange(nwg)
+        print("    lifetime by XCD (id %% 8): " + " ".join("%.1f" % np.median(lt[ids % 8 == x]) for x in range(8)))
+        print("    lifetime by 1/8 of the tile range: " + " ".join(
+            "%.1f" % np.median(lt[(ids // max(1, nwg // 8)) == x]) for x in range(8)))
+        print("    slowest 8 ids: %s" % list(np.argsort(lt)[-8:]))
+        return
     ok = dr > 0
     clk = np.median(dt[ok] / dr[ok]) * 100.0          # MHz
     tf = flops / ms / 1e9

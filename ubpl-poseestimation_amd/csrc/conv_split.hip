@@ -127,24 +127,50 @@ namespace {
 #ifndef UBPL_CLOCK_STAMP
 #define UBPL_CLOCK_STAMP 0
 #endif
+// Fair arbitration between the two workgroups a CU holds (UBPL_FAIRPRIO=1): the SIMD arbiter
+// favours the older wave, so the first-dispatched workgroup of a CU finishes ~20 % before the
+// second, which then runs alone (profiles/r05_v10_timeline.txt).  With this, every PERIOD K
+// steps the two swap s_setprio 1 / 0 (the younger = linear id in the grid's second half).
+#ifndef UBPL_FAIRPRIO
+#define UBPL_FAIRPRIO 0
+#endif
+template <int PERIOD>
+__device__ __forceinline__ void fair_prio(int step, bool younger) {
+    if (UBPL_FAIRPRIO && step % PERIOD == 0) {
+        if (((step / PERIOD) & 1) ^ (int)younger) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    }
+}
+
+// UBPL_CLOCK_STAMP=2: the absolute real-time counter at workgroup entry and at its exit (after
+// the epilogue stores are issued) instead — the launch's timeline (tools/clock_probe.py tl)
 #if UBPL_CLOCK_STAMP
 __device__ unsigned long long g_clk_stamp[2][1 << 16];
 #define UBPL_STAMP_BEGIN                                                   \
     const unsigned long long stamp_t0 = __builtin_amdgcn_s_memtime(),     \
                              stamp_r0 = __builtin_amdgcn_s_memrealtime();
+#define UBPL_STAMP_PUT(A, B_)                                                               \
+    if (threadIdx.x == 0) {                                                                 \
+        const int sb = (blockIdx.x + gridDim.x * blockIdx.y) & 0xffff;                      \
+        g_clk_stamp[0][sb] = (A);                                                           \
+        g_clk_stamp[1][sb] = (B_);                                                          \
+    }
 #define UBPL_STAMP_END                                                                      \
-    {                                                                                       \
+    if (UBPL_CLOCK_STAMP == 1) {                                                            \
         const unsigned long long t1 = __builtin_amdgcn_s_memtime(),                        \
                                  r1 = __builtin_amdgcn_s_memrealtime();                    \
-        if (threadIdx.x == 0) {                                                             \
-            const int sb = (blockIdx.x + gridDim.x * blockIdx.y) & 0xffff;                  \
-            g_clk_stamp[0][sb] = t1 - stamp_t0;                                             \
-            g_clk_stamp[1][sb] = r1 - stamp_r0;                                             \
-        }                                                                                   \
+        UBPL_STAMP_PUT(t1 - stamp_t0, r1 - stamp_r0)                                        \
+    }
+#define UBPL_STAMP_EXIT                                                                     \
+    if (UBPL_CLOCK_STAMP == 2) {                                                            \
+        (void)stamp_t0;                                                                     \
+        const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();                     \
+        UBPL_STAMP_PUT(stamp_r0, r1)                                                        \
     }
 #else
 #define UBPL_STAMP_BEGIN
 #define UBPL_STAMP_END
+#define UBPL_STAMP_EXIT
 #endif
 
 constexpr int NT = 256;
@@ -1252,7 +1278,9 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
         const int nk = G * 9;
         stage_h(0, 0);
         for (int a = 0; a < NA - 1 && a < nk; ++a) stage_a(a, a);
+        const bool younger = (blockIdx.x + gridDim.x * blockIdx.y) >= (gridDim.x * gridDim.y) / 2;
         for (int s = 0; s < nk; ++s) {
+            fair_prio<8>(s, younger);
             const int cg = s / 9, tap = s - cg * 9;
             if (NHB == 1 && HBAND && tap == 0 && cg > 0) {
                 // every wave done with group cg - 1: halo rows 2 .. R-1 (rows 0 and 1 came
@@ -1340,6 +1368,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
         out_base(obase, nok);
         store_tile<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, y, m0 + BM <= Cout && n0 + BNT <= N);
     }
+    UBPL_STAMP_EXIT
 }
 
 // ------------------------------------------------------------------ 1x1, split on load
@@ -1529,7 +1558,9 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     stage(0, 0);
     if (NS == 3 && nkt > 1) stage(1, 16);
     if (deepb && nkt > 1) stage_b(1, 16);
+    const bool younger = (blockIdx.x + gridDim.x * blockIdx.y) >= (gridDim.x * gridDim.y) / 2;
     for (int t = 0; t < nkt; ++t) {
+        fair_prio<2>(t, younger);
         // stage t landed for every wave (NS = 3: this wave's stage t+1 DMA may stay in
         // flight; deepb: B(t+1), issued after A(t), may stay in flight), every wave
         // done with stage t-1
@@ -1702,6 +1733,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         return;
     }
     store_tile<TM, TN>(acc, nok, obase, m0, M, P, y, m0 + BM <= M && n0 + BNT <= N);
+    UBPL_STAMP_EXIT
 }
 
 // ------------------------------------------------------------------ 1x1, split on load, warp-specialized (round 5)
