@@ -669,10 +669,12 @@ def test_psa_halo_kernel_matches_per_tap_kernel_bit_for_bit(case, teams, _lib_di
     assert esp <= 2 * e32 + 1e-8, (esp, e32)
 
 
+@pytest.mark.parametrize("mode", [4, 5])
 @pytest.mark.parametrize("case", HALO_CASES)
-def test_psa_halo_m16_kernel_vs_f64(case, _lib_dispatch):
+def test_psa_halo_m16_kernel_vs_f64(case, mode, _lib_dispatch):
     """The one-buffer halo kernel on 16x16x32 MFMAs (the six piece products paired
-    along K: a different summation order from the 32x32x16 kernels) — forward with
+    along K: a different summation order from the 32x32x16 kernels; mode 5: its
+    tap-pair form, two taps per chain on 64-row tiles) — forward with
     bias + residual and the data gradient on the first / last images within the
     split path's bar of float64 (2x the exact-f32 kernel's error), and within a
     few f32 ulps of the 32x32x16 one-buffer kernel everywhere."""
@@ -690,25 +692,25 @@ def test_psa_halo_m16_kernel_vs_f64(case, _lib_dispatch):
     wd = Kn.conv_weight_split(w32.to(DEV), 1, 3)
     dys = Kn.split_activation(dy32.to(DEV), 3, 1) if dy32 is not None else None
     outs = {}
-    for mode in (3, 4):
-        lib.ubpl_set_psa_dispatch(mode, -1)
+    for md in (3, mode):
+        lib.ubpl_set_psa_dispatch(md, -1)
         y = Kn.conv2d_forward_psa(xs, ws, b32.to(DEV), res=res32.to(DEV))
         dx = Kn.conv2d_forward_psa(dys, wd, None) if dys is not None else None
         torch.cuda.synchronize()
-        outs[mode] = (y, dx)
-    y3, y4 = outs[3][0], outs[4][0]
+        outs[md] = (y, dx)
+    y3, y4 = outs[3][0], outs[mode][0]
     assert bool(torch.isfinite(y4).all())
     assert float((y4 - y3).abs().max()) <= 1e-5 * float(y3.abs().max()), float((y4 - y3).abs().max())
     sl = [0, B - 1]
     yref = F.conv2d(x32[sl].double(), w32.double(), b32.double(), 1, 1) + res32[sl].double()
     y_f32 = Kn.conv2d_forward(x32[sl].to(DEV), w32.to(DEV), b32.to(DEV), 1, res=res32[sl].to(DEV))
     e32, e16, e3 = _rel(y_f32, yref), _rel(y4[sl], yref), _rel(y3[sl], yref)
-    print("halo m16 %s: f32 %.2e m16 %.2e 32x32 %.2e" % (case, e32, e16, e3))
+    print("halo m16 mode %d %s: f32 %.2e m16 %.2e 32x32 %.2e" % (mode, case, e32, e16, e3))
     assert e16 <= 2 * e32 + 1e-8, (e16, e32)
     if dys is not None:
         dxref = torch.nn.grad.conv2d_input((2, Cin, H, H), w32.double(), dy32[sl].double(), padding=1)
         dx32 = Kn.conv2d_dgrad(dy32[sl].to(DEV), w32.to(DEV))
-        e32d, e16d = _rel(dx32, dxref), _rel(outs[4][1][sl], dxref)
+        e32d, e16d = _rel(dx32, dxref), _rel(outs[mode][1][sl], dxref)
         print("halo m16 dgrad %s: f32 %.2e m16 %.2e" % (case, e32d, e16d))
         assert e16d <= 2 * e32d + 1e-8, (e16d, e32d)
 

@@ -954,7 +954,10 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
 // channels in the two k halves — so three 32-k MFMAs per 16 x 16 tile and K step, the same
 // MFMA cycles as six 32x32x16 per 32 x 32 tile.  The chip holds a higher clock on this shape
 // (the roofline kernel is DVFS-held: DESIGN §6 round 5); a 16 x 16 tile drains 4 adds.
-template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2, int BNT1 = 256, bool M16 = false>
+// PAIR (with M16, 64-row tiles): a K step is two taps of a channel group (the ninth alone), its
+// A image [piece][64 rows][64 B] holding both, so each 16x16 tile's chain is six MFMAs over 32
+// channels x 2 taps and drains once per two taps (half the adds); waves 32 rows x 128 pixels.
+template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2, int BNT1 = 256, bool M16 = false, bool PAIR = false>
 __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
@@ -969,8 +972,9 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
                                                // piece starts at HPX - 32, rewriting pixels it overlaps)
     constexpr int HTOT = NP * HI;
     constexpr int NH = (HTOT + NW - 1) / NW;   // halo DMA instructions per wave (spares repeat the last one)
-    constexpr int AB = NP * BM * 32;           // A bytes per K step
-    constexpr int AI = NP * BM / 32;           // A DMA instructions per K step (32 rows each)
+    constexpr int AB = NP * BM * (PAIR ? 64 : 32);   // A bytes per K step
+    constexpr int AI = AB / 1024;              // A DMA instructions per K step (1 KB each)
+    constexpr int TPG = PAIR ? 5 : 9;          // K steps per channel group
     constexpr int NAW = (AI + NW - 1) / NW;    // per wave (spares repeat the last one)
     // GS (the one-piece path): a stage is a whole channel group — its halo and the
     // nine taps' A images (one barrier per 9 K steps; 8 MFMAs per wave per K step
@@ -989,11 +993,13 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
     constexpr int NA1 = UBPL_PSAH_NA_MAX * AB + NP * HB <= 80 * 1024 ? UBPL_PSAH_NA_MAX
                         : (3 * AB + NP * HB <= 80 * 1024 ? 3 : 2);
     constexpr int NA = GS ? 9 * NS_G : (NHB == 1 ? NA1 : 3);   // A images
-    constexpr int WGM = BM / 64, WGN = 4 / WGM;
+    constexpr int WROWS = PAIR ? 32 : 64;      // rows of a wave tile
+    constexpr int WGM = BM / WROWS, WGN = 4 / WGM;
     constexpr int TM = 2, TN = BNT1 / WGN / 32;
-    constexpr int TM16 = 4, TN16 = BNT1 / WGN / 16;   // M16: 16 x 16 blocks of the 64-row wave tile
+    constexpr int TM16 = WROWS / 16, TN16 = BNT1 / WGN / 16;   // M16: 16 x 16 blocks of the wave tile
     static_assert(BM == 64 || BM == 128, "64- or 128-row tiles");
     static_assert(!M16 || (NP == 3 && TEAMS == 1 && NHB == 1), "M16: 6xbf16, one halo buffer");
+    static_assert(!PAIR || (M16 && BM == 64 && !UBPL_PSAH_BAND), "PAIR: M16, 64-row tiles");
     constexpr int OFF_H = NA * AB, LDS_BYTES = OFF_H + (GS ? NS_G : NHB) * NP * HB;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS");
     static_assert(BNT % WW == 0 && WW % 32 == 0, "whole rows of 32-pixel fragments");
@@ -1004,7 +1010,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
     const int Ktot = Cin * 9;
     // (wid wave-uniform in an SGPR: the DMA index math below stays scalar)
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = ((wid & 3) / WGN) * 64, wn = (wid >> 2) * BNT1 + ((wid & 3) % WGN) * (BNT1 / WGN);
+    const int wm = ((wid & 3) / WGN) * WROWS, wn = (wid >> 2) * BNT1 + ((wid & 3) % WGN) * (BNT1 / WGN);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int by = lam % gridDim.y, bx = lam / gridDim.y;
     const int m0 = by * BM;
@@ -1030,6 +1036,29 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(base + (int64_t)p * wplane * 2 + a_lane),
                                              (lds_ptr_t)dst, 16, 0, 0);
         }
+    };
+    // PAIR: the A image of K step s = taps (2j, 2j+1) of group cg (j = 4: tap 8, its 32 B
+    // loaded twice): row r's four 16-B chunks (c = 2 tap + half) at position c ^ ((r >> 2) & 3),
+    // 16 rows per instruction (lane: row lane / 4, position lane % 4)
+    auto stage_a2 = [&](int slot, int s) {
+        const int cg = s / TPG, j = s - cg * TPG;
+        const int k0 = cg * 144 + j * 32;
+        const int rl = lane >> 2, pos = lane & 3;
+#pragma unroll
+        for (int u = 0; u < NAW; ++u) {
+            const int i = min(u * NW + wid, AI - 1);   // (a spare repeats the last: same bytes)
+            const int p = i / (BM / 16), rb = i % (BM / 16);
+            const int row = 16 * rb + rl;
+            const int csrc = pos ^ ((row >> 2) & 3);
+            const int kk = k0 + 8 * (j == 4 ? (csrc & 1) : csrc);
+            const uint16_t* src = wp + (int64_t)p * wplane + (int64_t)min(m0 + row, Cout - 1) * Ktot + kk;
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(lds + slot * AB + p * BM * 64 + rb * 1024),
+                                             16, 0, 0);
+        }
+    };
+    auto stage_A = [&](int slot, int s) {
+        if constexpr (PAIR) stage_a2(slot, s);
+        else stage_a(slot, s);
     };
     // halo of group cg: instruction i = wid * NH + u (piece i / HI, 32-pixel chunk i % HI)
     auto stage_h = [&](int buf, int cg) {
@@ -1195,6 +1224,86 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             acc4[TM16 - 1][TN16 - 1][r] = v;
         }
     };
+    // PAIR K step: taps a (halo offset ta) and, when TWO, b (tb); per tile the chain
+    // P1a P1b P2a P2b P3a P3b from zero (P1 = hi.lo + lo.hi, P2 = hi.mid + mid.hi,
+    // P3 = mid.mid + hi.hi), one 4-add drain
+    auto step16p = [&](auto twoc, const char* abase, const char* hbase, int ta, int tb) {
+        constexpr bool TWO = decltype(twoc)::value;
+        constexpr int NT2 = TWO ? 2 : 1;
+        const int ch = kc & 1, yh = kc >> 1;
+        bf16x8 af[NT2][TM16][3];
+#pragma unroll
+        for (int i = 0; i < TM16; ++i) {
+            const int row = wm + 16 * i + c16;
+#pragma unroll
+            for (int h2 = 0; h2 < NT2; ++h2) {
+                const char* ar = abase + row * 64 + 16 * ((2 * h2 + ch) ^ ((row >> 2) & 3));
+                af[h2][i][0] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 2 : 0) * BM * 64);
+                af[h2][i][1] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 1 : 0) * BM * 64);
+                af[h2][i][2] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 0 : 1) * BM * 64);
+            }
+        }
+        const char* hb_a = hbase + ta * 32;
+        const char* hb_b = hbase + tb * 32;
+        auto read_b = [&](int j, bf16x8 (&bo)[NT2][2]) {
+#pragma unroll
+            for (int h2 = 0; h2 < NT2; ++h2) {
+                const char* br = (h2 ? hb_b : hb_a) + boff[j];
+                bo[h2][0] = *reinterpret_cast<const bf16x8*>(br + (yh ? 0 : 2) * HB);
+                bo[h2][1] = *reinterpret_cast<const bf16x8*>(br + (yh ? 0 : 1) * HB);
+            }
+        };
+        bf16x8 bc[NT2][2], bn[NT2][2];
+        read_b(0, bc);
+        const floatx4 zero = {};
+        floatx4 prev;
+#pragma unroll
+        for (int q = 0; q < TM16 * TN16; ++q) {
+            const int j = q / TM16, i = q % TM16;
+            if (i == 0 && j > 0) {
+#pragma unroll
+                for (int h2 = 0; h2 < NT2; ++h2) {
+                    bc[h2][0] = bn[h2][0];
+                    bc[h2][1] = bn[h2][1];
+                }
+            }
+            floatx4 cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i][0], bc[0][0], zero, 0, 0, 0);
+            if constexpr (TWO) cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i][0], bc[1][0], cur, 0, 0, 0);
+            cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i][1], bc[0][1], cur, 0, 0, 0);
+            if constexpr (TWO) cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i][1], bc[1][1], cur, 0, 0, 0);
+            cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i][2], bc[0][1], cur, 0, 0, 0);
+            if constexpr (TWO) cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i][2], bc[1][1], cur, 0, 0, 0);
+            const bool pf = i == 0 && j + 1 < TN16;
+            if (pf) read_b(j + 1, bn);
+            if (q > 0) {
+                const int pj = (q - 1) / TM16, pi = (q - 1) % TM16;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = acc4[pi][pj][r] + prev[r];
+                    asm("" : "+v"(v));
+                    acc4[pi][pj][r] = v;
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+                if (pf) __builtin_amdgcn_sched_group_barrier(0x100, 2 * NT2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+                if constexpr (TWO) __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            prev = cur;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = acc4[TM16 - 1][TN16 - 1][r] + prev[r];
+            asm("" : "+v"(v));
+            acc4[TM16 - 1][TN16 - 1][r] = v;
+        }
+    };
     auto step = [&](const char* abase, const char* hbase, int toff) {
         if constexpr (M16) {
             step16(abase, hbase, toff);
@@ -1275,13 +1384,13 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
     } else {
-        const int nk = G * 9;
+        const int nk = G * TPG;
         stage_h(0, 0);
-        for (int a = 0; a < NA - 1 && a < nk; ++a) stage_a(a, a);
+        for (int a = 0; a < NA - 1 && a < nk; ++a) stage_A(a, a);
         const bool younger = (blockIdx.x + gridDim.x * blockIdx.y) >= (gridDim.x * gridDim.y) / 2;
         for (int s = 0; s < nk; ++s) {
             fair_prio<8>(s, younger);
-            const int cg = s / 9, tap = s - cg * 9;
+            const int cg = s / TPG, tap = s - cg * TPG;   // (PAIR: tap = the pair index)
             if (NHB == 1 && HBAND && tap == 0 && cg > 0) {
                 // every wave done with group cg - 1: halo rows 2 .. R-1 (rows 0 and 1 came
                 // in at taps 3 and 6 of the previous group) now, waited for; rows R, R+1
@@ -1326,7 +1435,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             }
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            if (s + NA - 1 < nk) stage_a((s + NA - 1) % NA, s + NA - 1);
+            if (s + NA - 1 < nk) stage_A((s + NA - 1) % NA, s + NA - 1);
             if (NHB == 2 && tap == 0 && cg + 1 < G) stage_h((cg + 1) & 1, cg + 1);
             if constexpr (NHB == 1 && HBAND) {
                 if (tap == 0 && cg > 0)
@@ -1336,8 +1445,15 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
                 if (tap == 6 && cg + 1 < G)
                     stage_band(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, cg + 1);
             }
-            const int kh = tap / 3;
-            step(lds + (s % NA) * AB, lds + OFF_H + (NHB == 2 ? (cg & 1) : 0) * NP * HB, kh * W2 + (tap - 3 * kh));
+            if constexpr (PAIR) {
+                const int t0 = 2 * tap, t1 = t0 + 1;
+                const int off0 = (t0 / 3) * W2 + t0 % 3, off1 = (t1 / 3) * W2 + t1 % 3;
+                if (tap < 4) step16p(std::true_type{}, lds + (s % NA) * AB, lds + OFF_H, off0, off1);
+                else step16p(std::false_type{}, lds + (s % NA) * AB, lds + OFF_H, off0, off0);
+            } else {
+                const int kh = tap / 3;
+                step(lds + (s % NA) * AB, lds + OFF_H + (NHB == 2 ? (cg & 1) : 0) * NP * HB, kh * W2 + (tap - 3 * kh));
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
     }
@@ -3152,7 +3268,7 @@ extern "C" __attribute__((visibility("default"))) int ubpl_debug_clock_stamps(un
 #endif
 
 UBPL_API int ubpl_set_psa_dispatch(int halo_mode, int teams) {
-    if (halo_mode < -1 || halo_mode > 4 || teams < -1 || teams > 2) return (int)hipErrorInvalidValue;
+    if (halo_mode < -1 || halo_mode > 5 || teams < -1 || teams > 2) return (int)hipErrorInvalidValue;
     psa_dispatch();                       // the environment's values are read first, then replaced
     g_psa_halo.store(halo_mode);
     g_psa_teams.store(teams);
@@ -3229,7 +3345,7 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     // different summation order).  The tests compare the kernels in one process; modes 0-3
     // compute in the same order, bit for bit.
     const int halo_mode = psa_dispatch().halo;
-    const bool one_buf = npieces == 3 && (halo_mode == 3 || halo_mode == 4 || halo_mode < 0);
+    const bool one_buf = npieces == 3 && (halo_mode >= 3 || halo_mode < 0);
     // the 96-wide planes: 192-pixel tiles on 128 rows whatever the plan's row block (its
     // cost model is conv_psa_kernel's), the one-buffer variant only
     const bool w96 = W == 96 && Cout % 128 == 0 && H % 2 == 0 &&
@@ -3282,11 +3398,25 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         const dim3 grid((unsigned)(N / 256), (unsigned)mt);
         if (one_buf) {   // one halo buffer, two workgroups per CU
             // the 16x16x32 form (UBPL_PSAH16=1)
-            static const bool m16_env = [] {
+            // UBPL_PSAH16=1: the 16x16x32 form; 2: its tap-pair form on 64-row tiles
+            static const int m16_env = [] {
                 const char* e = std::getenv("UBPL_PSAH16");
-                return e != nullptr && std::atoi(e) != 0;
+                return e != nullptr ? std::atoi(e) : 0;
             }();
-            const bool m16 = halo_mode == 4 || (halo_mode < 0 && m16_env);
+            const bool pair = (halo_mode == 5 || (halo_mode < 0 && m16_env == 2)) && Cout % 64 == 0;
+            const bool m16 = halo_mode == 4 || (halo_mode < 0 && m16_env == 1);
+            if (pair) {
+                const dim3 grid64((unsigned)(N / 256), (unsigned)(Cout / 64));
+#define UBPL_PSAHP(W_)                                                                                          \
+    hipLaunchKernelGGL((conv_psah_kernel<W_, 3, 64, 1, 1, 256, true, true>), grid64, dim3(NT), 0, st, xs, xplane, \
+                       wsplit, wplane, bias, res, y, B, Cin, H, Cout)
+                if (W == 64) UBPL_PSAHP(64);
+                else if (W == 128) UBPL_PSAHP(128);
+                else UBPL_PSAHP(32);
+#undef UBPL_PSAHP
+                UBPL_LAUNCH_CHECK();
+                return 0;
+            }
 #define UBPL_PSAH1(W_, BM_)                                                                                   \
     do {                                                                                                      \
         if (m16)                                                                                              \
