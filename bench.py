@@ -213,8 +213,13 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config=
     # UBPL_PSA_HALO override (0: the per-tap conv_psa_kernel; 1: the double-buffered halo variant),
     # for which no traffic record exists
     halo = os.environ.get("UBPL_PSA_HALO", "")
-    pmc = pmc_traffic("psah") if config == "mt_ubpl" and halo == "" else None
-    if halo == "0":
+    m16 = os.environ.get("UBPL_PSAH16", "0") not in ("", "0")     # the opt-in 16x16x32 forms
+    pmc = pmc_traffic("psah") if config == "mt_ubpl" and halo == "" and not m16 else None
+    if m16 and halo != "0":
+        import re
+        desc = re.sub(r"conv_psah_kernel<[^>]*>", "conv_psah_kernel (UBPL_PSAH16=%s 16x16x32 variant)"
+                      % os.environ["UBPL_PSAH16"], desc)
+    elif halo == "0":
         import re
         desc = re.sub(r"conv_psah_kernel<[^>]*>", "conv_psa_kernel", desc).replace(
             ", input halo staged once per channel group", "").replace(", input halo staged once per channel "
