@@ -144,7 +144,7 @@ __device__ __forceinline__ void visit_chan4(int b0, int b1, int C, int c, int hw
     }
 }
 
-template <bool VEC>
+template <bool VEC, int U = 4>
 __global__ void __launch_bounds__(256) stats_kernel(const float* __restrict__ x, int B, int C, int HW, int bper,
                                                    double* __restrict__ part, unsigned* __restrict__ cnt,
                                                    StatsOut o) {
@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(256) stats_kernel(const float* __restrict__ x,
         // one accumulator, elements in the flattened loop's order (bit-identical
         // statistics); only the loads run ahead
         const float4* x4 = reinterpret_cast<const float4*>(x);
-        visit_chan4<4>(b0, b1, C, c, HW >> 2, [&](int, int64_t off) {
+        visit_chan4<U>(b0, b1, C, c, HW >> 2, [&](int, int64_t off) {
             const float4 v = x4[off];
             const float a = v.x - x0, q = v.y - x0, r = v.z - x0, d = v.w - x0;
             s1 += (a + q) + (r + d);
@@ -528,9 +528,16 @@ int splits_for(int B, int C) {
 // at least ~8k elements per (channel, slice) block — small planes get one
 // block per channel (at 4x4 / B=32, 2048 blocks of 32 elements each were pure
 // launch and ticket overhead).
+int bn_env(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e != nullptr ? atoi(e) : dflt;
+}
+
 int splits_for(int B, int C, int HW) {
     int s = splits_for(B, C);
-    const int64_t per_slice = (int64_t)B * HW / 8192;
+    // (tuning hook: UBPL_BN_MINSLICE elements per (channel, slice) block, default 8192)
+    static const int64_t minslice = bn_env("UBPL_BN_MINSLICE", 8192) > 0 ? bn_env("UBPL_BN_MINSLICE", 8192) : 8192;
+    const int64_t per_slice = (int64_t)B * HW / minslice;
     if (s > per_slice) s = per_slice > 1 ? (int)per_slice : 1;
     return s;
 }
@@ -691,7 +698,12 @@ UBPL_API int ubpl_bn_forward_stats(const float* x, int B, int C, int HW, const f
     part += CNT_DOUBLES;
     const StatsOut o{gamma, beta, eps, momentum, rmean, rvar, mean_out, invstd_out, scale, shift};
     const bool vec = (HW % 4 == 0) && (((uintptr_t)x & 15) == 0);
-    if (vec)
+    // (tuning hook: UBPL_BN_U=8: eight float4 loads in flight per thread instead of four)
+    static const bool u8 = bn_env("UBPL_BN_U", 4) == 8;
+    if (vec && u8)
+        hipLaunchKernelGGL((stats_kernel<true, 8>), dim3(C, gs), dim3(256), 0, (hipStream_t)stream, x, B, C, HW, bper,
+                           part, cnt, o);
+    else if (vec)
         hipLaunchKernelGGL(stats_kernel<true>, dim3(C, gs), dim3(256), 0, (hipStream_t)stream, x, B, C, HW, bper, part,
                            cnt, o);
     else
