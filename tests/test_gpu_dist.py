@@ -49,11 +49,11 @@ def _shard(obj, rows):
 ROWS = [[0, 2], [1, 3]]            # unlabeled rows 0-1, labeled rows 2-3 (TwoStreamBatchSampler order)
 
 
-def _setup(rows):
+def _setup(rows, case=CASE):
     from ubpl_amd.hourglass import StackedHourglass
     from ubpl_amd.optim import FlatAdamW
     from oracle import render as OR
-    cfg = seeds.step_cases()[CASE]
+    cfg = seeds.step_cases()[case]
     models, emas, _ = seeds.step_models(lambda k, s, m: StackedHourglass(k, s, m), cfg, device="cuda")
     optims = [FlatAdamW(m, lr=cfg["lr"], weight_decay=0) for m in models]
     loader, args = seeds.step_batch(cfg, OR.kps_heatmap_torch)
@@ -147,10 +147,10 @@ def test_dp_two_ranks_real_step(tmp_path, monkeypatch):
     np.testing.assert_allclose(flat(r0["rec"]), flat(recs[0]), rtol=1e-6)
 
 
-def _worker_graph(rank, world, port, out):
-    """Four MT_UBPL steps per rank, eager and then captured (2 eager warm-up
-    steps, the capture as graph segments around the two collectives, replays),
-    each from freshly seeded networks."""
+def _worker_graph(rank, world, port, out, case=CASE):
+    """Four MT_UBPL (or DualPose_UBPL) steps per rank, eager and then captured
+    (2 eager warm-up steps, the capture as graph segments around the two
+    collectives, replays), each from freshly seeded networks."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -163,10 +163,12 @@ def _worker_graph(rank, world, port, out):
         for mode in ("0", "1"):
             os.environ["UBPL_STEP_GRAPH"] = mode
             T._StepGraph.clear()
-            models, emas, optims, loader, args = _setup(ROWS[rank])
+            models, emas, optims, loader, args = _setup(ROWS[rank], case)
+            dual = seeds.step_cases()[case]["project"] == "DualPose_UBPL"
+            train, core = (T.train_dualpose_ubpl, T._dualpose_core) if dual else (T.train_mt_ubpl, T._mt_ubpl_core)
             with contextlib.redirect_stdout(io.StringIO()):
-                rec = T.train_mt_ubpl(loader * 4, models, emas, optims, args)
-            runner = T._StepGraph.get(T._mt_ubpl_core, models, emas, optims, args)
+                rec = train(loader * 4, models, emas, optims, args)
+            runner = T._StepGraph.get(core, models, emas, optims, args)
             torch.cuda.synchronize()
             res[mode] = {"rec": rec, "segments": len(runner.graph) if runner.graph else 0,
                          "params": [m.flat_params.cpu() for m in models + emas],
@@ -178,15 +180,17 @@ def _worker_graph(rank, world, port, out):
 
 
 @pytest.mark.timeout(300)
-def test_dp_two_ranks_segmented_graph_matches_eager(tmp_path):
+@pytest.mark.parametrize("case", ["mt_ubpl", "dualpose"])
+def test_dp_two_ranks_segmented_graph_matches_eager(tmp_path, case):
     """under torch.distributed the step is captured as
     graph segments (forward + losses | backward + merge | AdamW + EMA +
-    records) with the two collectives run eagerly between their replays.  Two
-    gloo ranks: after 4 steps every rank's networks, BN statistics and records
-    are bit-identical to its 4 eager steps, and the replicas agree."""
+    records) with the two collectives run eagerly between their replays, for
+    the MT_UBPL and the DualPose_UBPL steps.  Two gloo ranks: after 4 steps
+    every rank's networks, BN statistics and records are bit-identical to its
+    4 eager steps, and the replicas agree."""
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker_graph, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    procs = [ctx.Process(target=_worker_graph, args=(r, 2, port, str(tmp_path), case)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
