@@ -22,7 +22,7 @@ import sys
 
 PATS = {"f32": re.compile(r"conv_fwd_kernel<(\d+), 128, 3, 1, true, false"),
         "psa": re.compile(r"conv_psa_kernel<128, 3, 3, 256, 2(, false)?>"),
-        "psah": re.compile(r"conv_psah_kernel<64, 3, 128, 1, 1(, 256(, false)?)?>")}
+        "psah": re.compile(r"conv_psah_kernel<64, 3, 128, 1, 1(, 256(, false)*)?>")}
 # psa / psah: only the 512-workgroup launches (grid size in work-items)
 GRID = {"psa": 512 * 256, "psah": 512 * 256}
 PAT = PATS["f32"]
