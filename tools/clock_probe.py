@@ -24,6 +24,7 @@ from ubpl_amd import kernels as Kn  # noqa: E402
 
 SPLIT_PEAK = 2500.0 / 6          # f32-equivalent TF/s of 6 bf16 products at the dense bf16 peak
 TIMELINE = os.environ.get("UBPL_PROBE_TIMELINE") == "1"   # with a UBPL_CLOCK_STAMP=2 build
+PHASES = os.environ.get("UBPL_PROBE_PHASES") == "1"       # with a UBPL_CLOCK_STAMP=3 build
 
 
 def stamps(lib, n):
@@ -49,6 +50,24 @@ def probe(name, fn, nwg, flops, seconds, lib):
     ev1.record()
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / 20
+    if PHASES:
+        # UBPL_CLOCK_STAMP=3 build, 1x1 kernel only: per-workgroup K-loop phase sums (wave 0)
+        if "sol" not in name:
+            return
+        buf = (ctypes.c_ulonglong * (4 * nwg))()
+        assert lib.ubpl_debug_clock_stamps4(buf, nwg) == 0
+        a = np.frombuffer(buf, dtype=np.uint64).astype(np.float64).reshape(4, nwg)
+        med = np.median(a, axis=1)
+        tot = med.sum()
+        print("%-34s %.3f ms/launch; K-loop cycles per workgroup (median): wait+barrier %.0f (%.0f %%), DMA issue"
+              " %.0f (%.0f %%), prologue+split %.0f (%.0f %%), MFMA rows %.0f (%.0f %%); sum %.0f"
+              % (name, ms, med[0], 100 * med[0] / tot, med[1], 100 * med[1] / tot, med[2], 100 * med[2] / tot,
+                 med[3], 100 * med[3] / tot, tot))
+        ids = np.arange(nwg)
+        for half, sel in (("first half", ids < nwg // 2), ("second half", ids >= nwg // 2)):
+            m = np.median(a[:, sel], axis=1)
+            print("    %s: %s" % (half, " ".join("%.0f" % v for v in m)))
+        return
     dt, dr = stamps(lib, nwg)
     if TIMELINE:
         # UBPL_CLOCK_STAMP=2 build: absolute real-time (100 MHz) at workgroup entry / exit
@@ -80,7 +99,9 @@ def main():
     seconds = float(sys.argv[1]) if len(sys.argv) > 1 else 3.0
     lib = _lib.lib()
     if not hasattr(lib, "ubpl_debug_clock_stamps"):
-        raise SystemExit("not a UBPL_CLOCK_STAMP=1 build (set UBPL_LIB_DIR)")
+        raise SystemExit("not a UBPL_CLOCK_STAMP build (set UBPL_LIB_DIR)")
+    lib.ubpl_debug_clock_stamps4.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.ubpl_debug_clock_stamps4.restype = ctypes.c_int
     lib.ubpl_debug_clock_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.ubpl_debug_clock_stamps.restype = ctypes.c_int
     dev = torch.device("cuda", 0)

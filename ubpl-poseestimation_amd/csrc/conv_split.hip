@@ -110,6 +110,7 @@ namespace {
 #ifndef UBPL_SOL_APF
 #define UBPL_SOL_APF 0
 #endif
+
 // timing-only: conv1x1_sol_kernel's DMA ring, waits and barriers without the compute
 #ifndef UBPL_SOL_NOCOMP
 #define UBPL_SOL_NOCOMP 0
@@ -145,7 +146,7 @@ __device__ __forceinline__ void fair_prio(int step, bool younger) {
 // UBPL_CLOCK_STAMP=2: the absolute real-time counter at workgroup entry and at its exit (after
 // the epilogue stores are issued) instead — the launch's timeline (tools/clock_probe.py tl)
 #if UBPL_CLOCK_STAMP
-__device__ unsigned long long g_clk_stamp[2][1 << 16];
+__device__ unsigned long long g_clk_stamp[4][1 << 16];
 #define UBPL_STAMP_BEGIN                                                   \
     const unsigned long long stamp_t0 = __builtin_amdgcn_s_memtime(),     \
                              stamp_r0 = __builtin_amdgcn_s_memrealtime();
@@ -171,6 +172,16 @@ __device__ unsigned long long g_clk_stamp[2][1 << 16];
 #define UBPL_STAMP_BEGIN
 #define UBPL_STAMP_END
 #define UBPL_STAMP_EXIT
+#endif
+// UBPL_CLOCK_STAMP=3: conv1x1_sol_kernel's K-loop phases (shader clocks summed over the loop, wave
+// 0): DMA wait + barrier, DMA issue, prologue + split, MFMA rows — rows 0-3 of g_clk_stamp
+#if UBPL_CLOCK_STAMP == 3
+#define UBPL_PH(v)                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+    const unsigned long long v = __builtin_amdgcn_s_memtime();           \
+    __builtin_amdgcn_sched_barrier(0);
+#else
+#define UBPL_PH(v)
 #endif
 
 constexpr int NT = 256;
@@ -1675,7 +1686,11 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     if (NS == 3 && nkt > 1) stage(1, 16);
     if (deepb && nkt > 1) stage_b(1, 16);
     const bool younger = (blockIdx.x + gridDim.x * blockIdx.y) >= (gridDim.x * gridDim.y) / 2;
+#if UBPL_CLOCK_STAMP == 3
+    unsigned long long ph[4] = {0, 0, 0, 0};
+#endif
     for (int t = 0; t < nkt; ++t) {
+        UBPL_PH(p0)
         fair_prio<2>(t, younger);
         // stage t landed for every wave (NS = 3: this wave's stage t+1 DMA may stay in
         // flight; deepb: B(t+1), issued after A(t), may stay in flight), every wave
@@ -1690,6 +1705,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        UBPL_PH(p1)
         if (deepb) {
             // A(t+1) first, then B(t+2): the next wait leaves only B(t+2) in flight
             if (t + 1 < nkt) stage_a((t + 1) % NS, (t + 1) * 16);
@@ -1697,6 +1713,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         } else if (t + NS - 1 < nkt) {
             stage((t + NS - 1) % NS, (t + NS - 1) * 16);
         }
+        UBPL_PH(p2)
         if (UBPL_SOL_NOCOMP) continue;
         const int kt = t * 16;
         const char* base = lds + (t % NS) * AB;                       // A of stage t
@@ -1706,6 +1723,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         bf16x8 bfr[TN][NP];
 #pragma unroll
         for (int j = 0; j < TN; ++j) split_col(bbase, j, sc, sh, bfr[j]);
+        UBPL_PH(p3)
         if constexpr (NP == 1) {
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
@@ -1783,7 +1801,21 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
 #endif
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if UBPL_CLOCK_STAMP == 3
+        UBPL_PH(p4)
+        ph[0] += p1 - p0;
+        ph[1] += p2 - p1;
+        ph[2] += p3 - p2;
+        ph[3] += p4 - p3;
+#endif
     }
+#if UBPL_CLOCK_STAMP == 3
+    if (threadIdx.x == 0) {
+        const int sb = (blockIdx.x + gridDim.x * blockIdx.y) & 0xffff;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g_clk_stamp[q][sb] = ph[q];
+    }
+#endif
     UBPL_STAMP_END
 
     out_base(obase, nok);
@@ -3264,6 +3296,17 @@ extern "C" __attribute__((visibility("default"))) int ubpl_debug_clock_stamps(un
         e = hipMemcpyFromSymbol(out + n, HIP_SYMBOL(g_clk_stamp), sizeof(unsigned long long) * n,
                                 sizeof(unsigned long long) * (1 << 16), hipMemcpyDeviceToHost);
     return (int)e;
+}
+// (the same, rows 0-3: UBPL_CLOCK_STAMP=3's four phase sums)
+extern "C" __attribute__((visibility("default"))) int ubpl_debug_clock_stamps4(unsigned long long* out, int n) {
+    if (n < 0 || n > (1 << 16)) return (int)hipErrorInvalidValue;
+    for (int q = 0; q < 4; ++q) {
+        const hipError_t e = hipMemcpyFromSymbol(out + (int64_t)q * n, HIP_SYMBOL(g_clk_stamp),
+                                                 sizeof(unsigned long long) * n,
+                                                 sizeof(unsigned long long) * (1 << 16) * q, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
 }
 #endif
 
