@@ -9,6 +9,11 @@ Each kernel runs back to back on random data for `seconds` (the chip settles its
 under load: MI355X_MICROARCH.md 'DVFS give-back' item 6), then the last launch's per-
 workgroup stamps give clock = d(s_memtime) / d(s_memrealtime) x 100 MHz; printed with the
 launch time and the matrix-core rate it implies at 2.4 GHz and at the measured clock.
+
+Other stamp builds: EXTRA=-DUBPL_CLOCK_STAMP=2 with UBPL_PROBE_TIMELINE=1 — the launch
+timeline (workgroup entry / exit, by XCD and by dispatch half; profiles/r05_v10_timeline.txt);
+EXTRA=-DUBPL_CLOCK_STAMP=3 with UBPL_PROBE_PHASES=1 — the 1x1 kernel's K-loop phases
+(profiles/r05_v13_sol_phases.txt).
 """
 import ctypes
 import os
