@@ -336,3 +336,63 @@ def _graph_vs_eager(monkeypatch, case="mt_ubpl"):
     for a, b in zip(s_e, s_g):
         assert torch.equal(a, b), diag
     assert _flat(r_e, []) == _flat(r_g, [])
+
+
+def _rows(obj, rows):
+    """A batch restricted to some of its rows (every tensor whose first dim is the batch)."""
+    if torch.is_tensor(obj):
+        return obj[rows].clone() if obj.dim() and obj.shape[0] == 4 else obj
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_rows(v, rows) for v in obj)
+    if isinstance(obj, dict):
+        return {k: _rows(v, rows) for k, v in obj.items()}
+    return obj
+
+
+def test_step_graph_ragged_batch_and_new_epoch(monkeypatch):
+    """The captured step's other paths, against the same schedule run eagerly,
+    bit for bit: a batch of another shape mid-epoch (2 of the 4 rows: it runs
+    eagerly, and the full-size batches after it replay the graph again), then a
+    new epoch whose host constants change (learning rate halved, EMA epoch
+    advanced: the runner releases its graph and captures anew)."""
+    import contextlib
+    import io
+    from ubpl_amd import train as T
+    from ubpl_amd.optim import FlatAdamW
+    cfg = seeds.step_cases()["mt_ubpl"]
+    monkeypatch.setenv("UBPL_MODEL_STREAMS", "1")
+
+    def run(graph):
+        monkeypatch.setenv("UBPL_STEP_GRAPH", "1" if graph else "0")
+        T._StepGraph.clear()
+        models, emas, _ = seeds.step_models(_factory, cfg, device="cuda")
+        optims = [FlatAdamW(m, lr=cfg["lr"], weight_decay=0) for m in models]
+        loader, args = seeds.step_batch(cfg, OR.kps_heatmap_torch)
+        full = loader[0]
+        small = _rows(full, [0, 2])                 # one unlabeled, one labeled row
+        with contextlib.redirect_stdout(io.StringIO()):
+            r1 = T.train_mt_ubpl([full, full, full, small, full], models, emas, optims, args)
+            runner = T._StepGraph.get(T._mt_ubpl_core, models, emas, optims, args)
+            first = runner.graph
+            for o in optims:
+                o.param_groups[0]["lr"] *= 0.5
+            args.epo += 1
+            r2 = T.train_mt_ubpl([full] * 4, models, emas, optims, args)
+        runner = T._StepGraph.get(T._mt_ubpl_core, models, emas, optims, args)
+        if graph:
+            assert first is not None and runner.graph is not None and runner.graph is not first
+        else:
+            assert first is None and runner.graph is None
+        torch.cuda.synchronize()
+        out = ([m.flat_params.clone() for m in models + emas], [m.flat_stats.clone() for m in models + emas],
+               _flat([r1, r2], []))
+        T._StepGraph.clear()
+        return out
+
+    p_e, s_e, r_e = run(False)
+    p_g, s_g, r_g = run(True)
+    for a, b in zip(p_e, p_g):
+        assert torch.equal(a, b), float((a - b).abs().max())
+    for a, b in zip(s_e, s_g):
+        assert torch.equal(a, b), float((a - b).abs().max())
+    assert r_e == r_g
