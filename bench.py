@@ -227,14 +227,31 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config=
     elif halo:
         import re
         desc = re.sub(r"conv_psah_kernel<[^>]*>", "conv_psah_kernel (UBPL_PSA_HALO=%s variant)" % halo, desc)
+    # the clock the chip holds under this kernel (a probe of a diagnostic build, committed):
+    # the live rate against the peak at that clock, beside the nominal-clock frac
+    clk = clock_probe() if pmc is not None else None
+    if clk is not None:
+        clk = dict(clk, frac_at_clock=round(achieved / (peak * clk["clock_mhz"] / 2400.0), 4))
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": (pmc or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc,
+            "clock_probe": clk,
             "kernel": desc, "pieces": npieces,
             "flops_per_launch": flops, "launches_per_step": n, "avg_launch_us": round(avg_ms * 1e3, 2),
             "kernel_ms_per_step": round(per_step_ms, 3), "fits_in_step": consistent,
             "timing": "HIP events around back-to-back replays of the step's launches of this kernel "
                       "(standalone; inputs resident), after the timed region"}
+
+
+def clock_probe():
+    """The in-kernel clock measured under the default roofline kernel
+    (profiles/clock_probe_psah.json from tools/clock_probe.py); None if absent."""
+    p = os.path.join(ROOT, "profiles", "clock_probe_psah.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as fh:
+        d = json.load(fh)
+    return {"clock_mhz": d["clock_mhz"], "source": d.get("source"), "method": d.get("method")}
 
 
 def pmc_traffic(kind):
