@@ -36,7 +36,58 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "images/sec training step (MT_UBPL, 2-stack HG, 256×256) at 1/2/4/8 GPUs; PCK@0.2"
 MEANS = [0.4920829, 0.4920829, 0.4920829]
 F32_MFMA_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
-SPLIT6_PEAK_TFLOPS = 2500.0 / 6       # bf16 dense peak / 6 piece products per f32 product
+BF16_PEAK_TFLOPS = 2500.0             # dense bf16 / fp16 MFMA (the fp16 32x32x16 form takes the bf16 cycles)
+SPLIT6_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 6   # 6xbf16: 6 piece products per f32 product
+SPLIT3_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 3   # 2xfp16: 3 piece products per f32 product
+
+
+def piece_peak(npieces):
+    """f32-equivalent peak of a split conv with npieces per operand (the piece
+    products with pa + pb < npieces: 6 / 3 / 1 MFMAs per f32 product)."""
+    return {3: SPLIT6_PEAK_TFLOPS, 2: SPLIT3_PEAK_TFLOPS, 1: BF16_PEAK_TFLOPS}.get(npieces, F32_MFMA_PEAK_TFLOPS)
+
+
+def _conv(cin, cout, ks, hw):
+    return 2 * cin * cout * ks * ks * hw * hw
+
+
+def _residual(cin, cout, hw):
+    half = cout // 2
+    f = _conv(cin, half, 1, hw) + _conv(half, half, 3, hw) + _conv(half, cout, 1, hw)
+    return f + (_conv(cin, cout, 1, hw) if cin != cout else 0)
+
+
+def _hourglass(n, hw):
+    f = _residual(256, 256, hw) + 2 * _residual(256, 256, hw // 2)
+    return f + (_hourglass(n - 1, hw // 2) if n > 1 else _residual(256, 256, hw // 2))
+
+
+def forward_flops(S, K, res):
+    """Conv FLOP of one StackedHourglass forward per sample (models/pose/hourglass.py:12-99,
+    models/base/layers.py:53-111): 16.67 GF at HG2 256^2 K=16 — SURVEY.md §8d's 266.7 GF per
+    training sample = 16 forward-equivalents (2 students x 2 views x fwd + 2 bwd, 2 teachers x
+    2 views x fwd)."""
+    r2, r4 = res // 2, res // 4
+    f = _conv(3, 64, 7, r2) + _residual(64, 128, r2) + _residual(128, 128, r4) + _residual(128, 256, r4)
+    f += S * (_hourglass(4, r4) + _residual(256, 256, r4) + _conv(256, 256, 1, r4) + _conv(256, K, 1, r4))
+    return f + (S - 1) * (_conv(256, 256, 1, r4) + _conv(K, 256, 1, r4))
+
+
+def step_record(cfg, B, ms_per_step, precision):
+    """Step-level fraction of the matrix peak: the step's conv FLOP
+    (f32-equivalent; forward passes: 2 students x views + 2 teachers x views, backward =
+    2x forward) against the time the MFMA pipe would need at the precision's peaks
+    (2xfp16: forwards at the 3-product peak, gradients at the 6-product one)."""
+    F = forward_flops(cfg["S"], cfg["K"], cfg["res"]) * B
+    views = 1 if cfg["project"] == "DualPose_UBPL" else 2
+    fwd, bwd = 2 * views * F + 2 * views * F, 2 * views * 2 * F       # students' + teachers' forwards; gradients
+    pieces = {"f32": 0, "bf16": 1, "2xfp16": 2, "6xbf16": 3}[precision]
+    pf, pb = piece_peak(pieces), piece_peak(3 if pieces == 2 else pieces)
+    ideal_s = fwd / (pf * 1e12) + bwd / (pb * 1e12)
+    t = ms_per_step * 1e-3
+    return {"flop_per_step": fwd + bwd, "tflops": round((fwd + bwd) / t / 1e12, 2),
+            "step_frac": round(ideal_s / t, 4), "peak_tflops_fwd": round(pf, 1), "peak_tflops_bwd": round(pb, 1),
+            "note": "conv FLOP of the step (f32-equivalent) / step time, against the precision's MFMA peaks"}
 
 
 def make_args(B):
@@ -89,27 +140,33 @@ def make_batches(n, B, K, dev, seed, res=256, dualpose=False):
 
 
 ROOF_SHAPE = (128, 128, 3, 64, 64)   # Cin, Cout, KS, H, W of the roofline kernel's launches (headline)
-# per config: (Cin, Cout, KS, H, W) of the dominant conv_psa_kernel launches, pieces per operand, peak,
-# description.  HG8 at 384^2 runs its top hourglass level on 96x96 planes.
-ROOF = {
-    "mt_ubpl": ((128, 128, 3, 64, 64), 3, SPLIT6_PEAK_TFLOPS,
-                "conv_psah_kernel<64, 3, 128, 1, 1, 256> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad, input "
-                "halo staged once per channel group; 6xbf16 split-f32 MFMA; f32-equivalent FLOP/s, peak = bf16 "
-                "dense / 6)"),
-    "mt_ubpl_hg2_256_bf16": ((128, 128, 3, 64, 64), 1, 2500.0,
-                             "conv_psah_kernel<64, 1, 128, 2, 2, 256> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad, "
-                             "input halo staged once per channel group; bf16 operands, f32 accumulation; peak = "
-                             "bf16 dense MFMA)"),
-    "dualpose_hg4": ((128, 128, 3, 64, 64), 3, SPLIT6_PEAK_TFLOPS,
-                     "conv_psah_kernel<64, 3, 128, 1, 1, 256> (3x3 conv, 128->128 ch, 64x64 planes, fwd + dgrad; "
-                     "6xbf16; f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
-    "mt_ubpl_hg8_384": ((128, 128, 3, 96, 96), 3, SPLIT6_PEAK_TFLOPS,
-                        "conv_psah_kernel<96, 3, 128, 1, 1, 192> (3x3 conv, 128->128 ch, 96x96 planes, fwd + dgrad; 6xbf16; "
-                        "f32-equivalent FLOP/s, peak = bf16 dense / 6)"),
-    "mt_ubpl_hg8_384_bf16": ((128, 128, 3, 96, 96), 1, 2500.0,
-                             "conv_psa_kernel (3x3 conv, 128->128 ch, 96x96 planes, fwd + dgrad; bf16 operands, "
-                             "f32 accumulation; peak = bf16 dense MFMA)"),
-}
+# per config: (Cin, Cout, KS, H, W) of the dominant 3x3 conv launches (HG8 at 384^2 runs its top
+# hourglass level on 96x96 planes)
+ROOF = {"mt_ubpl": (128, 128, 3, 64, 64), "mt_ubpl_hg2_256_bf16": (128, 128, 3, 64, 64),
+        "dualpose_hg4": (128, 128, 3, 64, 64), "mt_ubpl_hg8_384": (128, 128, 3, 96, 96),
+        "mt_ubpl_hg8_384_bf16": (128, 128, 3, 96, 96)}
+
+
+def roof_kernel(shape, npieces):
+    """The instantiation ubpl_conv2d_forward_psa dispatches for these launches by default
+    (conv_split.hip): the input-halo kernel, one halo buffer and two workgroups per CU on the
+    split paths (<W, NP, 128, 1, 1, 256>; 96-wide planes: 192-pixel tiles), two teams on the
+    bf16 path at W <= 64; UBPL_PSA_HALO=0 / 1 (the only values the library accepts) select the
+    per-tap conv_psa_kernel / the double-buffered halo kernel."""
+    W = shape[4]
+    halo = os.environ.get("UBPL_PSA_HALO", "")
+    if halo == "0":
+        return "conv_psa_kernel<128, 3, %d, 256, 2> (per-tap B staging; UBPL_PSA_HALO=0)" % npieces
+    if halo == "1":
+        return "conv_psah_kernel<%d, %d, 128, ...> (double-buffered halo; UBPL_PSA_HALO=1)" % (W, npieces)
+    if npieces == 1:
+        return ("conv_psah_kernel<%d, 1, 128, 2, 2, 256>" % W) if W <= 64 else "conv_psa_kernel<128, 3, 1, 256, 2, 2>"
+    return "conv_psah_kernel<%d, %d, 128, 1, 1, %d>" % (W, npieces, 192 if W == 96 else 256)
+
+
+PIECE_NAME = {3: "6xbf16 split-f32 MFMA (3 bf16 pieces, 6 products)",
+              2: "2xfp16 split-f32 MFMA (2 fp16 pieces of the scaled operands, 3 products)",
+              1: "bf16 operands, f32 accumulation", 0: "exact f32 MFMA"}
 
 
 class PsaLaunches:
@@ -121,8 +178,8 @@ class PsaLaunches:
     256, 2> with UBPL_PSA_HALO=0), with no split-K slab — and keeps every
     tensor those pointers reference alive, so the launches can be replayed."""
 
-    def __init__(self, Kn, lib, shape=ROOF_SHAPE):
-        self.Kn, self.lib, self.shape = Kn, lib, tuple(shape)
+    def __init__(self, Kn, lib, shape=ROOF_SHAPE, npieces=None):
+        self.Kn, self.lib, self.shape, self.npieces = Kn, lib, tuple(shape), npieces
         self.calls, self.keep = [], []
 
     def __enter__(self):
@@ -137,7 +194,8 @@ class PsaLaunches:
 
         def psa(xs, ws, bias, res=None, out=None, stat_part=None, bwd=None):
             Cout, T, _ = ws.shape
-            rec._want = (xs.C, Cout, int(round(T ** 0.5)), xs.H, xs.W) == rec.shape
+            rec._want = (xs.C, Cout, int(round(T ** 0.5)), xs.H, xs.W) == rec.shape and \
+                rec.npieces in (None, ws.npieces)
             y = orig_psa(xs, ws, bias, res, out, stat_part, bwd)
             if rec._want:
                 rec.keep.append((xs, ws, bias, res, y, stat_part, bwd))
@@ -180,17 +238,23 @@ class PsaLaunches:
 
 def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config="mt_ubpl", train=None):
     """The dominant kernel: the 3x3 conv at the config's largest 3x3 planes
-    (headline: conv_psah_kernel<64,3,128,1,1>, the 3x3 conv on the 6xbf16 split
-    path at the 64x64 planes, forward + data gradient; the largest single entry
-    of the rocprofv3 kernel summary, profiles/r0*_summary).
-    achieved = algorithmic FLOP per launch (2*B*Cout*Cin*9*H*W; f32-equivalent
-    on the split path) / its average standalone launch duration (HIP events
-    around replayed launches, see PsaLaunches.time), vs the config's peak
-    (6xbf16: 2.5 PF bf16 dense / 6 piece products; bf16: 2.5 PF)."""
-    shape, npieces, peak, desc = ROOF[config]
+    (headline: the 3x3 128->128 conv at the 64x64 planes on the input-halo kernel;
+    the largest single entry of the rocprofv3 kernel summary, profiles/r0*_summary),
+    its launches at the precision's forward piece count (6xbf16: forward + data
+    gradient; 2xfp16: the forwards, whose data gradients run on 6xbf16).
+    achieved = algorithmic FLOP per launch (2*B*Cout*Cin*9*H*W; f32-equivalent on the
+    split paths) / its average standalone launch duration (HIP events around
+    replayed launches, see PsaLaunches.time), vs the pieces' peak (6xbf16: 2.5 PF
+    bf16 dense / 6 piece products; 2xfp16: / 3; bf16: 2.5 PF)."""
+    shape = ROOF[config]
+    npieces = Kn.conv_precision_pieces()
+    peak = piece_peak(npieces)
+    desc = "%s (3x3 conv, %d->%d ch, %dx%d planes, %s; %s; f32-equivalent FLOP/s, peak = bf16 dense / products)" % (
+        roof_kernel(shape, npieces), shape[0], shape[1], shape[3], shape[4],
+        "fwd + dgrad" if npieces != 2 else "fwd", PIECE_NAME[npieces])
     os.environ["UBPL_MODEL_STREAMS"] = "0"
     try:
-        with PsaLaunches(Kn, lib, shape) as rec, T._StepGraph.eager():
+        with PsaLaunches(Kn, lib, shape, npieces) as rec, T._StepGraph.eager():
             (train or T.train_mt_ubpl)([batch], models, emas, optims, args, verbose=False)
         torch.cuda.synchronize()
         avg_ms, n = rec.time()
@@ -209,33 +273,12 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config=
     if not consistent:
         print("bench: roofline kernel replays sum to %.2f ms > %.2f ms/step" % (per_step_ms, ms_per_step),
               file=sys.stderr)
-    # the kernel the dispatch picks: the default (profiles/pmc_roofline_psah.json measured it), or a
-    # UBPL_PSA_HALO override (0: the per-tap conv_psa_kernel; 1: the double-buffered halo variant),
-    # for which no traffic record exists
+    # HBM traffic by PMC (profiles/pmc_roofline_psah*.json) for the default dispatch of the headline
     halo = os.environ.get("UBPL_PSA_HALO", "")
-    m16 = os.environ.get("UBPL_PSAH16", "0") not in ("", "0")     # the opt-in 16x16x32 forms
-    pmc = pmc_traffic("psah") if config == "mt_ubpl" and halo == "" and not m16 else None
-    if m16 and halo != "0":
-        import re
-        desc = re.sub(r"conv_psah_kernel<[^>]*>", "conv_psah_kernel (UBPL_PSAH16=%s 16x16x32 variant)"
-                      % os.environ["UBPL_PSAH16"], desc)
-    elif halo == "0":
-        import re
-        desc = re.sub(r"conv_psah_kernel<[^>]*>", "conv_psa_kernel", desc).replace(
-            ", input halo staged once per channel group", "").replace(", input halo staged once per channel "
-                                                                      "group", "")
-    elif halo:
-        import re
-        desc = re.sub(r"conv_psah_kernel<[^>]*>", "conv_psah_kernel (UBPL_PSA_HALO=%s variant)" % halo, desc)
-    # the clock the chip holds under this kernel (a probe of a diagnostic build, committed):
-    # the live rate against the peak at that clock, beside the nominal-clock frac
-    clk = clock_probe() if pmc is not None else None
-    if clk is not None:
-        clk = dict(clk, frac_at_clock=round(achieved / (peak * clk["clock_mhz"] / 2400.0), 4))
+    pmc = pmc_traffic("psah%s" % ("" if npieces == 3 else npieces)) if config == "mt_ubpl" and halo == "" else None
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 2),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": (pmc or {}).get("hbm_bytes_per_launch"), "traffic_detail": pmc,
-            "clock_probe": clk,
             "kernel": desc, "pieces": npieces,
             "flops_per_launch": flops, "launches_per_step": n, "avg_launch_us": round(avg_ms * 1e3, 2),
             "kernel_ms_per_step": round(per_step_ms, 3), "fits_in_step": consistent,
@@ -243,23 +286,11 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config=
                       "(standalone; inputs resident), after the timed region"}
 
 
-def clock_probe():
-    """The in-kernel clock measured under the default roofline kernel
-    (profiles/clock_probe_psah.json from tools/clock_probe.py); None if absent."""
-    p = os.path.join(ROOT, "profiles", "clock_probe_psah.json")
-    if not os.path.exists(p):
-        return None
-    with open(p) as fh:
-        d = json.load(fh)
-    return {"clock_mhz": d["clock_mhz"], "source": d.get("source"), "method": d.get("method")}
-
-
 def pmc_traffic(kind):
     """HBM bytes per launch of the roofline kernel, measured by rocprofv3 --pmc
     passes over this bench command (tools/gpu_pmc.sh bench ->
     tools/pmc_roofline.py -> profiles/pmc_roofline[_psa].json); None if absent."""
-    p = os.path.join(ROOT, "profiles", {"psa": "pmc_roofline_psa.json", "psah": "pmc_roofline_psah.json"}.get(
-        kind, "pmc_roofline.json"))
+    p = os.path.join(ROOT, "profiles", "pmc_roofline_%s.json" % kind)
     if not os.path.exists(p):
         return None
     with open(p) as fh:
@@ -470,7 +501,8 @@ def main():
                        "per_gpu_batch": B, "input": "%dx%dx3" % (res, res),
                        "heatmap": "%dx%dx%d" % (K, res // 4, res // 4), "parallelism": "dp%d" % world,
                        "baseline_config": cfg["desc"]},
-            "roofline": roof, "cpu_baseline": cpu, "pck": pck_record() if headline else None,
+            "roofline": roof, "step": step_record(cfg, B, dt / a.steps * 1e3, Kn.conv_precision_name()),
+            "cpu_baseline": cpu, "pck": pck_record() if headline else None,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

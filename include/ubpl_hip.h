@@ -214,14 +214,19 @@ int ubpl_wgrad_slab_reduce(const float* slab, int splits, int Cout, int Cin, int
 /*@ src:f32[?] dst:f32[?] table:i64[nseg*5] */
 int ubpl_conv_weights_relayout(const float* src, float* dst, const int64_t* table, int nseg, int mode, void* stream);
 
-/* Split-bf16 MFMA path of the same Conv (conv_split.hip): every f32 operand
- * carried as npieces (2 or 3) bf16 pieces, the piece products with
- * pa + pb < npieces summed by v_mfma_f32_32x32x16_bf16 in f32.  Weights:
- * ubpl_conv_weights_split writes npieces bf16 planes (`plane` elements apart)
+/* Split MFMA path of the same Conv (conv_split.hip): every f32 operand carried
+ * as npieces 16-bit pieces, the piece products with pa + pb < npieces summed by
+ * the 32x32x16 MFMA in f32: npieces 3 = three bf16 pieces ("6xbf16", exact
+ * operands, 6 products), 2 = two fp16 pieces of the operand times a power-of-two
+ * scale ("2xfp16", 3 products on v_mfma_f32_32x32x16_f16; weights scaled by
+ * 2^(9 + ceil(log2 sqrt K)) for contraction length K, activations by 32, the
+ * accumulators unscaled exactly before the stores), 1 = bf16 operands.  Weights:
+ * ubpl_conv_weights_split writes npieces planes (`plane` elements apart)
  * of the mode-0 (forward, grouped tap-major) or mode-1 (data-gradient) layout
  * for many convs in one launch (table as above, dst_off % 8 == 0).
- * ubpl_conv2d_forward_split: (KS, stride) in {(1,1), (3,1)}, Cin % 16 == 0,
- * wsplit 16-B aligned; other arguments as ubpl_conv2d_forward. */
+ * ubpl_conv2d_forward_split (the register-staged kernel, npieces 3): (KS, stride)
+ * in {(1,1), (3,1)}, Cin % 16 == 0, wsplit 16-B aligned; other arguments as
+ * ubpl_conv2d_forward. */
 /*@ src:f32[?] dst:u16[npieces*plane] table:i64[nseg*5] */
 int ubpl_conv_weights_split(const float* src, uint16_t* dst, int64_t plane, const int64_t* table, int nseg, int mode,
                             int npieces, void* stream);
@@ -231,22 +236,24 @@ int ubpl_conv2d_forward_split(const float* x, int B, int Cin, int H, int W, cons
                               const float* bias, int Cout, int KS, int stride, const float* pscale,
                               const float* pshift, const float* res, float* y, int Ho, int Wo, float* slab,
                               int npieces, void* stream);
-/* Pre-split activations ("PSA"): npieces bf16 planes (`plane` elements apart)
+/* Pre-split activations ("PSA"): npieces 16-bit planes (`plane` elements apart)
  * of [B][C/16][H+2pad][W+2pad][16] holding relu(x*pscale + pshift) (or x when
- * pscale is null) with a zero border; C % 16 == 0. */
-/*@ x:f32[(int64_t)B*C*H*W] pscale:f32[C] pshift:f32[C] dst:u16[(npieces-1)*plane+(int64_t)B*C*(H+2*pad)*(W+2*pad)] */
+ * pscale is null) with a zero border; C % 16 == 0.  npieces 2 (2xfp16): the
+ * pieces of v * 32; dst3 (nullable, npieces 2 only): also the 3-piece bf16
+ * image of v (planes `plane3` apart) from the same read. */
+/*@ x:f32[(int64_t)B*C*H*W] pscale:f32[C] pshift:f32[C] dst:u16[(npieces-1)*plane+(int64_t)B*C*(H+2*pad)*(W+2*pad)] dst3:u16[2*plane3+(int64_t)B*C*(H+2*pad)*(W+2*pad)] */
 int ubpl_split_activation(const float* x, int B, int C, int H, int W, const float* pscale, const float* pshift,
-                          int pad, int npieces, uint16_t* dst, int64_t plane, void* stream);
+                          int pad, int npieces, uint16_t* dst, int64_t plane, uint16_t* dst3, int64_t plane3,
+                          void* stream);
 /* Stride-1 conv (KS 1 or 3) of PSA activations (pad >= (KS-1)/2) with split
  * weights: both operands DMA'd global -> LDS; y = conv + bias (+ res, may alias y). */
 int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int KS, int H, int W, int npieces);
 /* Test hook (host-only): the 3x3 input-halo kernel dispatch of
  * ubpl_conv2d_forward_psa.  halo_mode -1 default, 0 off, 1 on where eligible,
  * 2 on and required (an ineligible 3x3 launch returns hipErrorInvalidValue),
- * 3 the one-buffer variant required, 4 the one-buffer variant on 16x16x32
- * MFMAs (paired piece products) required; teams -1 default, 1 / 2 teams per
+ * 3 the one-buffer variant required; teams -1 default, 1 / 2 teams per
  * workgroup.  The environment (UBPL_PSA_HALO = 0 / 1, UBPL_PSA_TEAMS) sets the
- * initial values, read once. */
+ * initial values, read once; (-2, -2) returns to the environment's values. */
 int ubpl_set_psa_dispatch(int halo_mode, int teams);
 /* 3x3 weight gradient (+ bias gradient, db nullable) on the split path from PSA
  * operands with a 1-pixel border: dys = split(dy), xs = split(conv input),
@@ -297,11 +304,11 @@ int ubpl_stem_s2d_split(const float* x, int B, int C, int H, int W, int pad, int
 /*@ w:f32[(int64_t)Cout*C*KS*KS] dst:u16[(npieces-1)*plane+(int64_t)Cout*256] */
 int ubpl_stem_weight_s2d_split(const float* w, int Cout, int C, int KS, int npieces, uint16_t* dst, int64_t plane,
                                void* stream);
-/* 1x1 stride-1 conv on the 6xbf16 path with the f32 activations split while
+/* 1x1 stride-1 conv on the split path with the f32 activations split while
  * they are staged (no pre-split image): y = conv(relu(x*pscale + pshift) or x)
- * + bias (+ res, may alias y); wsplit = 3 planes of [Cout][Cin] from
- * ubpl_conv_weights_split (KS = 1); npieces 3 = 6xbf16, 1 = bf16 operands (one
- * plane; no epilogue partials).  Cin % 16 == 0, Cout % 16 == 0, P % 4 == 0.
+ * + bias (+ res, may alias y); wsplit = npieces planes of [Cout][Cin] from
+ * ubpl_conv_weights_split (KS = 1); npieces 3 = 6xbf16, 2 = 2xfp16 (no epilogue
+ * partials), 1 = bf16 operands (one plane; no epilogue partials).  Cin % 16 == 0, Cout % 16 == 0, P % 4 == 0.
  * stat_part (nullable): BatchNorm partials of y (ubpl_bn_partials layout).
  * _preferred: 1 when the shape is supported and fills the chip. */
 int ubpl_conv1x1_split_load_preferred(int B, int Cin, int Cout, int P);

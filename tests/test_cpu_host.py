@@ -91,9 +91,9 @@ def test_torch_ops_check_arguments_before_the_call():
     plane = B * C * (H + 2) * (W + 2)
     dst = torch.zeros(npieces * plane, dtype=torch.int16)
     with pytest.raises(RuntimeError, match="dst holds"):
-        ops.split_activation(torch.zeros(B * C * H * W), B, C, H, W, None, None, pad, npieces, dst[:-1], plane)
+        ops.split_activation(torch.zeros(B * C * H * W), B, C, H, W, None, None, pad, npieces, dst[:-1], plane, None, 0)
     with pytest.raises(RuntimeError, match="expected a device tensor"):
-        ops.split_activation(torch.zeros(B * C * H * W), B, C, H, W, None, None, pad, npieces, dst, plane)
+        ops.split_activation(torch.zeros(B * C * H * W), B, C, H, W, None, None, pad, npieces, dst, plane, None, 0)
     # an integer output of the wrong type
     with pytest.raises(RuntimeError, match="out_cnt must be i32"):
         ops.loss_finalize(0, torch.zeros(8), None, None, None, None, 0, 0, 2, 1, 4, 0.5, torch.zeros(1),
@@ -511,3 +511,37 @@ def test_step_generator_collectives_in_order(monkeypatch):
     assert not hasattr(T, "_AR_OVERLAP")
     rec = open(os.path.join(os.path.dirname(__file__), "..", "profiles", "r05_rccl_packed_fp32.txt")).read()
     assert "runTreeUpDown<float, FuncSum<float>" in rec
+
+
+def test_zero_pseudo_count_raises_like_the_reference():
+    """projects/MT_UBPL.py:292-293 (and DualPose_UBPL.py:212-213) divide the selected
+    pseudo-label count by the pseudo-label count, both Python ints, in the batch line:
+    a step with none raises ZeroDivisionError.  The HIP step's records raise the same
+    when they are consumed (one step late, train._LaggedRecords), whether or not the
+    line is printed; with counts the rate is the reference's."""
+    from types import SimpleNamespace
+    from ubpl_amd import train as T
+    from ubpl_amd.losses import AvgCounter
+    M, K = 2, 16
+    args = SimpleNamespace(pseudoScoreThr=0.95)
+    cnt = lambda: [AvgCounter() for _ in range(M)]   # noqa: E731
+
+    def mt(n_ps, verbose):
+        nrec = 3 * M + 1
+        host = [0.1] * nrec + [4, n_ps, 0] * M + [2] + [0.5] * K     # per model [pec_n, epc_n, n_sel], 1 FDL view
+        T._mt_ubpl_records(host, 0, (1, 64, 4, 3 * M + 1, True), M, cnt(), cnt(), cnt(), AvgCounter(), args,
+                           verbose)
+    for verbose in (False, True):
+        with pytest.raises(ZeroDivisionError):
+            mt(0, verbose)
+        mt(3, verbose)
+    assert T._pseudo_rate(3, 6) == 0.5
+
+    def dual(c_ps, verbose):
+        nrec = 3 * M + 1
+        host = [0.1] * nrec + [4, 4, 5, c_ps, 1, 2] * M + [2] + [0.5] * (2 * K)
+        T._dualpose_records(host, 0, 6 * M + 1, K, True, 1, M, 4, cnt(), cnt(), cnt(), AvgCounter(), args, verbose)
+    for verbose in (False, True):
+        with pytest.raises(ZeroDivisionError):
+            dual(0, verbose)
+        dual(7, verbose)

@@ -147,23 +147,32 @@ def test_dp_two_ranks_real_step(tmp_path, monkeypatch):
     np.testing.assert_allclose(flat(r0["rec"]), flat(recs[0]), rtol=1e-6)
 
 
-def _worker_graph(rank, world, port, out, case=CASE):
+def _worker_graph(rank, world, port, out, case=CASE, backend="gloo"):
     """Four MT_UBPL (or DualPose_UBPL) steps per rank, eager and then captured
     (2 eager warm-up steps, the capture as graph segments around the two
-    collectives, replays), each from freshly seeded networks."""
+    collectives, replays), each from freshly seeded networks.  backend "nccl"
+    (RCCL): one rank with the distributed path forced on (UBPL_DIST_WORLD1)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    if backend == "nccl":
+        os.environ["UBPL_DIST_WORLD1"] = "1"
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import contextlib
         import io
         from ubpl_amd import train as T
+        from ubpl_amd import dist as D
+        assert D.is_dist()
         res = {}
         for mode in ("0", "1"):
             os.environ["UBPL_STEP_GRAPH"] = mode
             T._StepGraph.clear()
-            models, emas, optims, loader, args = _setup(ROWS[rank], case)
+            models, emas, optims, loader, args = _setup(ROWS[rank] if world > 1 else [0, 1, 2, 3], case)
             dual = seeds.step_cases()[case]["project"] == "DualPose_UBPL"
             train, core = (T.train_dualpose_ubpl, T._dualpose_core) if dual else (T.train_mt_ubpl, T._mt_ubpl_core)
             with contextlib.redirect_stdout(io.StringIO()):
@@ -205,3 +214,29 @@ def test_dp_two_ranks_segmented_graph_matches_eager(tmp_path, case):
         assert r["0"]["rec"] == r["1"]["rec"]
     for a, b in zip(rs[0]["1"]["params"], rs[1]["1"]["params"]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("case", ["mt_ubpl", "dualpose"])
+def test_rccl_segmented_graph_matches_eager(tmp_path, case):
+    """the captured step under torch.distributed on the backend that runs
+    it in production, RCCL ("nccl"): one rank (RCCL takes one rank per device; the
+    box has one GPU) with the distributed path forced on, so both collectives run
+    through RCCL between the segment replays — ProcessGroupNCCL's watchdog thread
+    beside the thread_local captures, the synchronous all-reduce ordered between
+    replays, recordStream on tensors of the graph's pool.  After 4 steps the
+    captured run (3 segments) equals the eager run bit for bit: networks, BN
+    statistics and records."""
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_worker_graph, args=(0, 1, _free_port(), str(tmp_path), case, "nccl"))
+    p.start()
+    p.join(timeout=240)
+    assert p.exitcode == 0
+    r = torch.load(os.path.join(tmp_path, "graph_rank0.pt"), weights_only=True)
+    assert r["0"]["segments"] == 0 and r["1"]["segments"] == 3
+    for what in ("params", "stats"):
+        for a, b in zip(r["0"][what], r["1"][what]):
+            assert torch.equal(a, b), what
+    assert r["0"]["rec"] == r["1"]["rec"]

@@ -40,7 +40,7 @@ def _forwards(models, imgs, streams):
     return outs
 
 
-@pytest.mark.parametrize("precision", ["3xbf16", "6xbf16"])
+@pytest.mark.parametrize("precision", ["2xfp16", "6xbf16"])
 def test_network_forwards_on_four_streams_repeat_bit_for_bit(precision):
     """Four train-mode HG2 forwards (B=32, 256x256, two views each), one HIP
     stream per network as the training step runs them, repeated on the same

@@ -188,8 +188,9 @@ def test_hourglass(case):
 
 
 # ---------------------------------------------------------------- T1
-# the B=32 headline step takes ~1 min of CPU: pinned here only with UBPL_SLOW=1
-# (the GPU suite runs the oracle at B=32 on the GPU host and checks it there)
+# the B=32 headline step takes ~2 min of CPU: pinned here only with UBPL_SLOW=1 (passed in
+# rounds 5 and 6).  The GPU suite checks the HIP step at B=32 against the reference's own
+# fixtures (tests/golden/steps.npz / steps64.npz records, test_gpu_train.py), not the oracle.
 _STEP_CASES = [pytest.param(c, marks=pytest.mark.skipif(seeds.step_cases()[c]["B"] > 8 and
                                                         os.environ.get("UBPL_SLOW") != "1",
                                                         reason="slow CPU case (UBPL_SLOW=1)"))

@@ -89,9 +89,11 @@ inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // GROUPED: a scheduling barrier after each fragment's 16 loads (their
 // addresses die once issued) — keeps the widest tiles (conv_psa 128 x 256)
 // within 256 VGPRs without scratch.
+// sc: the scale of the accumulators (a power of two: the 2xfp16 path's operand
+// scales, see split2; 1 elsewhere) — the seed is (bias + res) * sc, exactly.
 template <int TM, int TN, bool GROUPED = false, typename ACC>
 __device__ __forceinline__ void seed_acc(ACC (&acc)[TM][TN], const float* bias, const float* res,
-                                         const int64_t (&obase)[TN], int mrow0, int M, int P) {
+                                         const int64_t (&obase)[TN], int mrow0, int M, int P, float sc = 1.f) {
     const int h = (threadIdx.x & 63) >> 5;
     if (res != nullptr) {
         const bool hb = bias != nullptr;
@@ -107,7 +109,7 @@ __device__ __forceinline__ void seed_acc(ACC (&acc)[TM][TN], const float* bias, 
                 for (int r = 0; r < 16; ++r) {
                     const int m = min(mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
                     const float bv = bp[m];
-                    acc[i][j][r] = (hb ? bv : 0.f) + rj[m * P];
+                    acc[i][j][r] = ((hb ? bv : 0.f) + rj[m * P]) * sc;
                 }
                 if (GROUPED) __builtin_amdgcn_sched_barrier(0);
             }
@@ -116,7 +118,7 @@ __device__ __forceinline__ void seed_acc(ACC (&acc)[TM][TN], const float* bias, 
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float bv = bias[min(mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1)];
+                const float bv = bias[min(mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1)] * sc;
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j][r] = bv;
             }
@@ -130,10 +132,35 @@ __device__ __forceinline__ void seed_acc(ACC (&acc)[TM][TN], const float* bias, 
     }
 }
 
-// Two floats -> NP packed bf16 pairs (piece p of a in the low half): the
-// split-bf16 representation v = v0 + v1 (+ v2), v_p = bf16(v - v_0 - ... - v_{p-1}).
+// Two floats -> NP packed 16-bit pairs (piece p of a in the low half).
+// NP = 3 (6xbf16) and 1 (bf16): the split-bf16 representation v = v0 + v1 (+ v2),
+// v_p = bf16(v - v_0 - ... - v_{p-1}) — three bf16 pieces carry an f32 exactly.
+// NP = 2 (2xfp16): two IEEE fp16 pieces, v = f16(v) + f16(v - f16(v)) to <= 2^-22
+// relative (two 11-bit significands), the piece products hi.hi + hi.lo + lo.hi exact
+// in f32: operands within a few f32 ulps with 3 MFMA products instead of 6.  fp16's exponent range is narrow
+// (normal from 2^-14, max 65504), so the callers pass values pre-scaled by a power
+// of two that puts them there (conv_split.hip: FP16_ACT_SCALE, fp16_wscale) and
+// undo the scale exactly on the accumulators.
+constexpr float FP16_ACT_SCALE = 32.f;   // activations: |v| up to 2047 without overflow, full
+                                         // precision from |v| >= 2^-7 (below: absolute error <= 2^-30)
+// weights of a GEMM with contraction length K (Cin * taps): 2^(9 + ceil(log2 sqrt K)), so
+// the default init's bound 1/sqrt(K) lands at 2^9 .. 2^10 (64x headroom to the fp16 max)
+__host__ __device__ __forceinline__ float fp16_wscale(int K) {
+    int e = 0;
+    while ((1 << (2 * e)) < K) ++e;            // 2^e >= sqrt(K)
+    return (float)(1 << (9 + e));
+}
 template <int NP>
 __device__ __forceinline__ void split2(float a, float b, uint32_t (&o)[NP]) {
+    if constexpr (NP == 2) {
+        typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+        const _Float16 ha = (_Float16)a, hb = (_Float16)b;
+        const f16x2_t v0 = {ha, hb};
+        const f16x2_t v1 = {(_Float16)(a - (float)ha), (_Float16)(b - (float)hb)};
+        o[0] = __builtin_bit_cast(uint32_t, v0);
+        o[1] = __builtin_bit_cast(uint32_t, v1);
+        return;
+    }
     typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -150,12 +177,12 @@ __device__ __forceinline__ void split2(float a, float b, uint32_t (&o)[NP]) {
 // 16 channel values of one pixel -> the NP bf16 planes of a PSA image row
 // (conv_split.hip split_act_kernel layout): 32 contiguous bytes per plane.
 template <int NP>
-__device__ __forceinline__ void store_psa_row(const float (&v)[16], uint16_t* d, int64_t plane) {
+__device__ __forceinline__ void store_psa_row(const float (&v)[16], uint16_t* d, int64_t plane, float sc = 1.f) {
     uint32_t pk[NP][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         uint32_t o[NP];
-        split2<NP>(v[2 * i], v[2 * i + 1], o);
+        split2<NP>(v[2 * i] * sc, v[2 * i + 1] * sc, o);
 #pragma unroll
         for (int p = 0; p < NP; ++p) pk[p][i] = o[p];
     }

@@ -27,165 +27,27 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short short8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
-#ifndef UBPL_PSA_PP
-#define UBPL_PSA_PP 1
-#endif
-#ifndef UBPL_PSA_PRIO
-#define UBPL_PSA_PRIO 0
-#endif
-// timing-only diagnostics (wrong or less exact results): no chunked accumulation / no K-step barrier
-#ifndef UBPL_PSA_NOCHUNK
-#define UBPL_PSA_NOCHUNK 0
-#endif
-#ifndef UBPL_PSA_NOWAIT
-#define UBPL_PSA_NOWAIT 0
-#endif
-#ifndef UBPL_PSA_NOSTORE
-#define UBPL_PSA_NOSTORE 0
-#endif
-#ifndef UBPL_SOL_NOSTORE
-#define UBPL_SOL_NOSTORE 0
-#endif
-// diagnostic: the 1x1 split-load kernel's scalar-epilogue stores as non-temporal stores
-#ifndef UBPL_SOL_NT_STORE
-#define UBPL_SOL_NT_STORE 0
-#endif
+// the unguarded epilogues' stores non-temporal (UBPL_NT_EPI, below); the 1x1 split-load kernel's
+// transposed residual epilogue (UBPL_SOL_TEPI); its launch-bounds occupancy (UBPL_SOL_LB); the
+// one-buffer halo kernel's deepest A ring (UBPL_PSAH_NA_MAX) — build-time knobs, defaults measured
+// (DESIGN.md §4, §6).  Round 6: the timing-only diagnostic builds and the variants that measured
+// slower (the warp-specialized 1x1 and 3x3 kernels, the 16x16x32 halo forms, fair arbitration,
+// clock stamps) were removed from the product source; they stay in the git history.
 #ifndef UBPL_SOL_TEPI
 #define UBPL_SOL_TEPI 1
 #endif
-#ifndef UBPL_PSA_NOBAR
-#define UBPL_PSA_NOBAR 0
-#endif
-// timing-only: conv_psa_kernel with no LDS-DMA at all (the compute loop on stale LDS) /
-// with no compute (the DMA ring, its waits and barriers only)
-#ifndef UBPL_PSA_NODMA
-#define UBPL_PSA_NODMA 0
-#endif
-#ifndef UBPL_PSA_NOCOMP
-#define UBPL_PSA_NOCOMP 0
-#endif
-// timing-only: the compute loop's fragments made in registers instead of read from LDS
-#ifndef UBPL_PSA_NOREAD
-#define UBPL_PSA_NOREAD 0
-#endif
-// the one-buffer halo kernel's banded refill (build-time, opt-in: measured slower, 213-257
-// vs 211-251 us)
-#ifndef UBPL_PSAH_BAND
-#define UBPL_PSAH_BAND 0
-#endif
-// the one-buffer halo kernel's deepest A ring (stages) where the LDS allows
 #ifndef UBPL_PSAH_NA_MAX
 #define UBPL_PSAH_NA_MAX 3
-#endif
-// timing-only: the one-buffer halo kernel without its per-group halo reload (stale halo)
-#ifndef UBPL_PSAH_NORELOAD
-#define UBPL_PSAH_NORELOAD 0
-#endif
-#ifndef UBPL_SOL_NOCHUNK
-#define UBPL_SOL_NOCHUNK 0
-#endif
-#ifndef UBPL_SOL_NOSPLIT
-#define UBPL_SOL_NOSPLIT 0
-#endif
-#ifndef UBPL_SOL_ACONTIG
-#define UBPL_SOL_ACONTIG 0
-#endif
-#ifndef UBPL_PSA_DMA_IL
-#define UBPL_PSA_DMA_IL 0
-#endif
-#ifndef UBPL_SOL_PP
-#define UBPL_SOL_PP 0
 #endif
 #ifndef UBPL_SOL_LB
 #define UBPL_SOL_LB 2
 #endif
-#ifndef UBPL_SOL_LDS_COEF
-#define UBPL_SOL_LDS_COEF 1
-#endif
-// conv1x1_sol_kernel's A (weight) fragment reads: 0 each row block's at its head, 1 the
-// same without the scheduling barrier between row blocks, 2 one row block ahead
-#ifndef UBPL_SOL_APF
-#define UBPL_SOL_APF 0
-#endif
-
-// timing-only: conv1x1_sol_kernel's DMA ring, waits and barriers without the compute
-#ifndef UBPL_SOL_NOCOMP
-#define UBPL_SOL_NOCOMP 0
-#endif
-// timing-only: conv1x1_sol_kernel's compute on stale LDS, no DMA; 1: none, 2: no weight
-// DMA (activations only), 3: half the activation rows' DMA (weights all)
-#ifndef UBPL_SOL_NODMA
-#define UBPL_SOL_NODMA 0
-#endif
-
-// diagnostic build only (UBPL_CLOCK_STAMP=1): conv_psah_kernel and conv1x1_sol_kernel record
-// per workgroup the shader-clock and the 100 MHz real-time counter deltas from entry to the
-// epilogue (lane 0 of wave 0, plain vector stores into a buffer of their own); the in-kernel
-// clock is their ratio x 100 MHz (ubpl_debug_clock_stamps, tools/clock_probe.py)
-#ifndef UBPL_CLOCK_STAMP
-#define UBPL_CLOCK_STAMP 0
-#endif
-// Fair arbitration between the two workgroups a CU holds (UBPL_FAIRPRIO=1): the SIMD arbiter
-// favours the older wave, so the first-dispatched workgroup of a CU finishes ~20 % before the
-// second, which then runs alone (profiles/r05_v10_timeline.txt).  With this, every PERIOD K
-// steps the two swap s_setprio 1 / 0 (the younger = linear id in the grid's second half).
-#ifndef UBPL_FAIRPRIO
-#define UBPL_FAIRPRIO 0
-#endif
-template <int PERIOD>
-__device__ __forceinline__ void fair_prio(int step, bool younger) {
-    if (UBPL_FAIRPRIO && step % PERIOD == 0) {
-        if (((step / PERIOD) & 1) ^ (int)younger) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-    }
-}
-
-// UBPL_CLOCK_STAMP=2: the absolute real-time counter at workgroup entry and at its exit (after
-// the epilogue stores are issued) instead — the launch's timeline (tools/clock_probe.py tl)
-#if UBPL_CLOCK_STAMP
-__device__ unsigned long long g_clk_stamp[4][1 << 16];
-#define UBPL_STAMP_BEGIN                                                   \
-    const unsigned long long stamp_t0 = __builtin_amdgcn_s_memtime(),     \
-                             stamp_r0 = __builtin_amdgcn_s_memrealtime();
-#define UBPL_STAMP_PUT(A, B_)                                                               \
-    if (threadIdx.x == 0) {                                                                 \
-        const int sb = (blockIdx.x + gridDim.x * blockIdx.y) & 0xffff;                      \
-        g_clk_stamp[0][sb] = (A);                                                           \
-        g_clk_stamp[1][sb] = (B_);                                                          \
-    }
-#define UBPL_STAMP_END                                                                      \
-    if (UBPL_CLOCK_STAMP == 1) {                                                            \
-        const unsigned long long t1 = __builtin_amdgcn_s_memtime(),                        \
-                                 r1 = __builtin_amdgcn_s_memrealtime();                    \
-        UBPL_STAMP_PUT(t1 - stamp_t0, r1 - stamp_r0)                                        \
-    }
-#define UBPL_STAMP_EXIT                                                                     \
-    if (UBPL_CLOCK_STAMP == 2) {                                                            \
-        (void)stamp_t0;                                                                     \
-        const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();                     \
-        UBPL_STAMP_PUT(stamp_r0, r1)                                                        \
-    }
-#else
-#define UBPL_STAMP_BEGIN
-#define UBPL_STAMP_END
-#define UBPL_STAMP_EXIT
-#endif
-// UBPL_CLOCK_STAMP=3: conv1x1_sol_kernel's K-loop phases (shader clocks summed over the loop, wave
-// 0): DMA wait + barrier, DMA issue, prologue + split, MFMA rows — rows 0-3 of g_clk_stamp
-#if UBPL_CLOCK_STAMP == 3
-#define UBPL_PH(v)                                                      \
-    __builtin_amdgcn_sched_barrier(0);                                   \
-    const unsigned long long v = __builtin_amdgcn_s_memtime();           \
-    __builtin_amdgcn_sched_barrier(0);
-#else
-#define UBPL_PH(v)
-#endif
 
 constexpr int NT = 256;
-constexpr bool PSA_WS = false;   // conv_psa_kernel 128 x 256 tiles, 6xbf16: warp-specialized variant (opt-in, measured no gain: DESIGN §6)
 constexpr int PSA_KSUB1 = 2;     // conv_psa_kernel on the bf16 path: 16-k steps per stage (measured)
 constexpr int SOL_PRO_K = 512;   // conv1x1_sol_kernel: largest input channel count with a prologue
 constexpr int BK = 32;
@@ -195,13 +57,24 @@ using ubpl::split2;
 
 __device__ __forceinline__ int swz(int row, int c) { return c ^ ((row >> 2) & 3); }
 
+// One 32x32x16 piece product: bf16 pieces (NP = 1, 3) or fp16 pieces (NP = 2, the
+// 2xfp16 path: common.h split2); the fragments travel as 16-bit lanes either way.
+template <int NP>
+__device__ __forceinline__ floatx16 mfma_piece(const bf16x8 a, const bf16x8 b, const floatx16 c) {
+    if constexpr (NP == 2)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), c,
+                                                      0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
 // acc += sum over piece pairs (pa, pb), pa + pb < NP, smallest terms first
 template <int NP>
 __device__ __forceinline__ void mfma_split(floatx16& acc, const bf16x8 (&a)[NP], const bf16x8 (&b)[NP]) {
 #pragma unroll
     for (int d = NP - 1; d >= 0; --d)
 #pragma unroll
-        for (int pa = d; pa >= 0; --pa) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa], b[d - pa], acc, 0, 0, 0);
+        for (int pa = d; pa >= 0; --pa) acc = mfma_piece<NP>(a[pa], b[d - pa], acc);
 }
 
 // acc += t one element at a time.  The floatx16 `+=` lowers to v_pk_add_f32,
@@ -219,17 +92,32 @@ __device__ __forceinline__ void drain(floatx16& acc, const floatx16 t) {
     }
 }
 
+// Ping-pong schedule of one chunk chain (its NP(NP+1)/2 MFMAs) with the previous
+// tile's 16 drain adds spread over the MFMA gaps (6 x (1 MFMA : 3 VALU) for the
+// 6-product chain, 3 x (1 : 6) for the 3-product one)
+template <int NP>
+__device__ __forceinline__ void pp_schedule() {
+    constexpr int NMF = NP * (NP + 1) / 2;
+    constexpr int NV = (16 + NMF - 1) / NMF;
+#pragma unroll
+    for (int g = 0; g < NMF; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // the same sum started from zero (one 16-k chunk of the chunked accumulation):
 // the first MFMA takes C = 0 as an inline constant, no zeroed registers
 template <int NP>
 __device__ __forceinline__ floatx16 mfma_split0(const bf16x8 (&a)[NP], const bf16x8 (&b)[NP]) {
     const floatx16 zero = {};
-    floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[NP - 1], b[0], zero, 0, 0, 0);
+    floatx16 t = mfma_piece<NP>(a[NP - 1], b[0], zero);
 #pragma unroll
     for (int d = NP - 1; d >= 0; --d)
 #pragma unroll
         for (int pa = d; pa >= 0; --pa)
-            if (!(d == NP - 1 && pa == NP - 1)) t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa], b[d - pa], t, 0, 0, 0);
+            if (!(d == NP - 1 && pa == NP - 1)) t = mfma_piece<NP>(a[pa], b[d - pa], t);
     return t;
 }
 
@@ -245,10 +133,11 @@ __device__ __forceinline__ floatx16 mfma_split0(const bf16x8 (&a)[NP], const bf1
 #ifndef UBPL_NT_EPI
 #define UBPL_NT_EPI 1
 #endif
+// inv: 1 / the accumulators' scale (seed_acc), applied exactly (a power of two)
 template <int TM, int TN>
 __device__ __forceinline__ void store_tile(const floatx16 (&acc)[TM][TN], const bool (&nok)[TN],
                                            const int64_t (&obase)[TN], int mrow0, int M, int P, float* y,
-                                           bool full) {
+                                           bool full, float inv = 1.f) {
     const int h = (threadIdx.x & 63) >> 5;
     if (full) {
 #pragma unroll
@@ -258,8 +147,8 @@ __device__ __forceinline__ void store_tile(const floatx16 (&acc)[TM][TN], const 
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     float* d = y + obase[j] + (int64_t)(mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h) * P;
-                    if (UBPL_NT_EPI) __builtin_nontemporal_store(acc[i][j][r], d);
-                    else *d = acc[i][j][r];
+                    if (UBPL_NT_EPI) __builtin_nontemporal_store(acc[i][j][r] * inv, d);
+                    else *d = acc[i][j][r] * inv;
                 }
         return;
     }
@@ -271,7 +160,7 @@ __device__ __forceinline__ void store_tile(const floatx16 (&acc)[TM][TN], const 
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = mrow0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m < M) y[obase[j] + (int64_t)m * P] = acc[i][j][r];
+                if (m < M) y[obase[j] + (int64_t)m * P] = acc[i][j][r] * inv;
             }
     }
 }
@@ -514,11 +403,14 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_split_kernel(
 // a K step, and a 3x3 tap is a constant offset (no bounds checks in the conv).
 // v = relu(x*scale + shift) (PRO) or x, then split; the border stays 0 (the
 // reference pads the BN+ReLU output: models/base/layers.py:45-50).
-template <int NP, bool PRO>
+// NP = 2 (2xfp16): the pieces of v * asc.  DUAL: also the 3-piece 6xbf16 image of v into dst3
+// (the 2xfp16 forward's conv input, kept for the 6xbf16 weight gradient: one read, two images).
+template <int NP, bool PRO, bool DUAL = false>
 __global__ void __launch_bounds__(256) split_act_kernel(const float* __restrict__ x, int C, int H, int W,
                                                        const float* __restrict__ pscale,
                                                        const float* __restrict__ pshift, int pad,
-                                                       uint16_t* __restrict__ dst, int64_t plane) {
+                                                       uint16_t* __restrict__ dst, int64_t plane, float asc,
+                                                       uint16_t* __restrict__ dst3, int64_t plane3) {
     const int Hp = H + 2 * pad, Wp = W + 2 * pad, G = C >> 4;
     const int b = blockIdx.z, g = blockIdx.y;
     const int pix = blockIdx.x * 256 + threadIdx.x;
@@ -537,7 +429,9 @@ __global__ void __launch_bounds__(256) split_act_kernel(const float* __restrict_
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) v[j] = in ? v[j] : 0.f;
-    ubpl::store_psa_row<NP>(v, dst + (((int64_t)(b * G + g) * Hp + hp) * Wp + wq) * 16, plane);
+    const int64_t o = (((int64_t)(b * G + g) * Hp + hp) * Wp + wq) * 16;
+    ubpl::store_psa_row<NP>(v, dst + o, plane, NP == 2 ? asc : 1.f);
+    if constexpr (DUAL) ubpl::store_psa_row<3>(v, dst3 + o, plane3);
 }
 
 // ------------------------------------------------------------------ the stem on the split path
@@ -624,18 +518,14 @@ __device__ __forceinline__ void vm_wait() {
 // KSUB: 16-k steps per stage and barrier (1; 2-4 on the one-piece bf16 path,
 // whose single MFMA per tile per 16-k step left the loop bound by the ring's
 // barriers and waits: KSUB steps of MFMAs between two barriers)
-// WS (warp-specialized, 512 threads): waves 0-3 compute (the 4-wave tile as
-// below), waves 4-7 only move the operands (the same DMA pieces, one loader per
-// compute wave's share) through a 4-stage ring, 2 K steps ahead; one barrier per
-// K step retires a stage.  A compute wave issues no DMA and waits on no vmcnt:
-// its SIMD partner is the loader, not a second MFMA-dense wave.
-template <int BM, int KS, int NP, int BNT = 128, int WGM = 2, bool EPI = false, int KSUB = 1, bool WS = false>
-__global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
+template <int BM, int KS, int NP, int BNT = 128, int WGM = 2, bool EPI = false, int KSUB = 1>
+__global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
                                                         int B, int Cin, int H, int W, int pad, int Cout, int kchunk,
                                                         float* __restrict__ slab, float* __restrict__ stat_part,
-                                                        ubpl::BnBwdEpi bwd) {
+                                                        ubpl::BnBwdEpi bwd, float osc) {
+    // osc: the accumulators' scale (2xfp16: weight scale x activation scale; 1 otherwise)
     constexpr int PADK = KS / 2;   // odd KS: centred; even KS (the stem, 4x4): taps -KS/2 .. KS/2 - 1
     constexpr int T = KS * KS;
     // waves: WGM along the output channels x 4/WGM along the pixels (64-row
@@ -645,8 +535,7 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
     constexpr int AB = NP * BM * 32, BB = NP * BNT * 32;   // bytes per stage
     // 128-pixel tiles: 3-stage ring; 256-pixel tiles (wave tile 64 x 128, twice
     // the MFMAs per barrier and per fragment byte): 2 stages, 2 workgroups per CU
-    constexpr int NS = WS ? 4 : (BNT == 256 ? 2 : 3);
-    static_assert(!WS || (BM == 128 && BNT == 256 && KSUB == 1 && !EPI), "warp-specialized: the 128 x 256 tile");
+    constexpr int NS = BNT == 256 ? 2 : 3;
     constexpr int BQ = BNT / 128;                          // B DMA instructions per wave per piece
     constexpr int SB = AB + BB;                            // one 16-k step's image
     __shared__ __attribute__((aligned(16))) char lds[NS * KSUB * SB];
@@ -656,8 +545,7 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
     const int Ktot = Cin * T;
     // (wid wave-uniform in an SGPR: the DMA index math stays scalar)
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool loader = WS && wid >= 4;
-    const int dw = WS ? (wid & 3) : wid;                   // the wave's share of the DMA pieces
+    const int dw = wid;                                    // the wave's share of the DMA pieces
     const int wm = (wid / WGN) * (BM / WGM), wn = (wid % WGN) * (BNT / WGN);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                               gridDim.x * gridDim.y * gridDim.z);
@@ -711,7 +599,6 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
     };
     // stage sb: its KSUB 16-k steps (those before k_end)
     auto stage = [&](int buf, int sb) {
-        if (UBPL_PSA_NODMA) return;
 #pragma unroll
         for (int u = 0; u < KSUB; ++u) {
             const int kt = k_begin + (sb * KSUB + u) * 16;
@@ -724,30 +611,6 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
 
     const int nk16 = (k_end - k_begin) >> 4;               // 16-k steps
     const int nkt = (nk16 + KSUB - 1) / KSUB;              // stages
-    if (UBPL_PSA_NODMA) {
-        // (the ring filled once with a run-time value, so the loads are not folded)
-        const uint32_t fill = __float_as_uint(bias ? bias[0] : 0.f) & 0x3f3f3f3fu;
-        for (int o = tid * 16; o < (int)sizeof(lds); o += (WS ? 2 * NT : NT) * 16)
-            *reinterpret_cast<uint4*>(lds + o) = make_uint4(fill, fill ^ o, fill, fill);
-        __syncthreads();
-    }
-    if constexpr (WS) {
-        if (loader) {
-            // stage t+3 into the slot the compute waves finished with before
-            // barrier t; before barrier t, stage t has landed (t+1, t+2 may not)
-            for (int sb = 0; sb < NS - 1 && sb < nkt; ++sb) stage(sb, sb);
-            for (int t = 0; t < nkt; ++t) {
-                const int ahead = min(NS - 2, nkt - 1 - t);
-                if (ahead >= 2) vm_wait<2 * NDMA>();
-                else if (ahead == 1) vm_wait<NDMA>();
-                else vm_wait<0>();
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-                if (t + NS - 1 < nkt) stage((t + NS - 1) % NS, t + NS - 1);
-            }
-            return;
-        }
-    }
 
     // accumulators start at bias (+ residual): see conv.hip conv_fwd_kernel
     const int li = lane & 31, h = lane >> 5;
@@ -764,32 +627,25 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
     }
     floatx16 acc[TM][TN];
     const bool direct = slab == nullptr;
-    ubpl::seed_acc<TM, TN, true>(acc, direct ? bias : nullptr, direct ? res : nullptr, obase, m0 + wm, Cout, P);
+    ubpl::seed_acc<TM, TN, true>(acc, direct ? bias : nullptr, direct ? res : nullptr, obase, m0 + wm, Cout, P, osc);
+    const float inv = 1.f / osc;
 
-    if (!WS && nkt > 0) stage(0, 0);
-    if (!WS && NS == 3 && nkt > 1) stage(1, 1);
+    if (nkt > 0) stage(0, 0);
+    if (NS == 3 && nkt > 1) stage(1, 1);
     for (int t = 0; t < nkt; ++t) {
         // retire stage t (this wave's DMA), then the barrier: every wave's
         // stage t has landed and every wave is done reading stage t-1
-        if constexpr (!WS) {
-            if (NS == 3 && t + 1 < nkt && (KSUB == 1 || (t + 2) * KSUB <= nk16)) {
-                if (a_issue) vm_wait<KSUB * (NP + BQ * NP)>();
-                else vm_wait<KSUB * BQ * NP>();
-            } else {
-                if (!UBPL_PSA_NOWAIT) vm_wait<0>();
-            }
+        if (NS == 3 && t + 1 < nkt && (KSUB == 1 || (t + 2) * KSUB <= nk16)) {
+            if (a_issue) vm_wait<KSUB * (NP + BQ * NP)>();
+            else vm_wait<KSUB * BQ * NP>();
+        } else {
+            vm_wait<0>();
         }
-        if (!UBPL_PSA_NOBAR) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        // UBPL_PSA_DMA_IL: the ping-pong body issues the next stage's DMA pieces
-        // between its MFMA chains instead of all of them ahead of the first chain
-        constexpr bool IL = UBPL_PSA_DMA_IL && NP == 3 && TN > 2 && UBPL_PSA_PP && KSUB == 1 && !WS;
-        const bool do_stage = !WS && t + NS - 1 < nkt;
-        const int sbuf = (t + NS - 1) % NS, skt = k_begin + (t + NS - 1) * 16;
-        if (!IL && do_stage) stage(sbuf, t + NS - 1);
+        if (t + NS - 1 < nkt) stage((t + NS - 1) % NS, t + NS - 1);
 #pragma unroll
         for (int u = 0; u < KSUB; ++u) {
-        if (UBPL_PSA_NOCOMP) break;
         if (KSUB > 1 && (t * KSUB + u) >= nk16) break;
         const int cur = t % NS;
         const char* base = lds + (cur * KSUB + u) * SB;
@@ -798,11 +654,6 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
             const int row = wn + 32 * j + li;
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
-                if (UBPL_PSA_NOREAD) {
-                    const uint32_t q = 0x3f003f00u + (uint32_t)((t * 7 + row + p) & 255);
-                    bfr[j][p] = __builtin_bit_cast(bf16x8, make_uint4(q, q ^ 1, q ^ 2, q ^ 3));
-                    continue;
-                }
                 bfr[j][p] = *reinterpret_cast<const bf16x8*>(base + AB + p * BNT * 32 + row * 32 +
                                                             16 * (h ^ ((row >> 3) & 1)));
             }
@@ -812,68 +663,30 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
             const int row = wm + 32 * i + li;
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
-                if (UBPL_PSA_NOREAD) {
-                    const uint32_t q = 0x3f003f00u + (uint32_t)((t * 5 + row + p) & 255);
-                    af[i][p] = __builtin_bit_cast(bf16x8, make_uint4(q, q ^ 4, q ^ 5, q ^ 6));
-                    continue;
-                }
                 af[i][p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
             }
         }
-        if constexpr (NP == 3 && TN > 2 && UBPL_PSA_PP && !UBPL_PSA_NOCHUNK) {
+        if constexpr (NP == 3 && TN > 2) {
             // ping-pong chunks: tile q's 6-MFMA chain is issued with tile q-1's
             // 16 drain adds between its MFMAs (3 VALU slots per MFMA gap), so the
             // adds hide in the matrix pipe's gaps instead of trailing each chain
 #pragma unroll
             for (int j = 0; j < TN / 2; ++j) read_b(j);
             __builtin_amdgcn_sched_barrier(0);
-            if (UBPL_PSA_PRIO) __builtin_amdgcn_s_setprio(1);
             floatx16 prev = mfma_split0<NP>(af[0], bfr[0]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = TN / 2; j < TN; ++j) read_b(j);
-            constexpr int NQ = TM * TN - 1;   // chains after the first: DMA slots
 #pragma unroll
             for (int q = 1; q < TM * TN; ++q) {
                 const int j = q / TM, i = q % TM, pj = (q - 1) / TM, pi = (q - 1) % TM;
                 const floatx16 cur = mfma_split0<NP>(af[i], bfr[j]);
-                if (IL && do_stage) {
-#pragma unroll
-                    for (int d = q - 1; d < NDMA; d += NQ) stage_piece(sbuf, skt, d);
-                }
                 drain(acc[pi][pj], prev);
-#pragma unroll
-                for (int g = 0; g < 6; ++g) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
+                pp_schedule<NP>();
                 prev = cur;
             }
             drain(acc[TM - 1][TN - 1], prev);
-            if (UBPL_PSA_PRIO) __builtin_amdgcn_s_setprio(0);
-        } else if constexpr (NP == 3 && TN > 2 && !UBPL_PSA_NOCHUNK) {
-            // (no register room for every tile's chunk at once)  The B fragments
-            // come in two halves: 18 reads in flight overflow the 4-bit lgkm
-            // counter and the compiler then waits for ALL of them before the first
-            // MFMA; with A + half of B (12) it waits for the first tile's operands
-            // only, and the second half is read behind the first column's MFMAs.
-#pragma unroll
-            for (int j = 0; j < TN / 2; ++j) read_b(j);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < TM; ++i) drain(acc[i][0], mfma_split0<NP>(af[i], bfr[0]));
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = TN / 2; j < TN; ++j) read_b(j);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 1; j < TN; ++j)
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    drain(acc[i][j], mfma_split0<NP>(af[i], bfr[j]));
-                }
-        } else if constexpr (NP == 3 && !UBPL_PSA_NOCHUNK) {
+        } else if constexpr (NP == 3) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) read_b(j);
             // every tile's chunk chain first, the f32 adds after them (behind a
@@ -915,24 +728,14 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (m < Cout) sl[(int64_t)m * N + n] = acc[i][j][r];
+                    if (m < Cout) sl[(int64_t)m * N + n] = acc[i][j][r] * inv;
                 }
         }
         return;
     }
     if (EPI && stat_part) ubpl::tile_bn_partials<TM, TN>(acc, nok, m0 + wm, Cout, n0 + wn, N, stat_part);
     if (EPI && bwd.part) ubpl::tile_bn_bwd_partials<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, n0 + wn, N, bwd);
-    if (UBPL_PSA_NOSTORE) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if (nok[j] && acc[i][j][r] == 1234.5f) y[obase[j]] = acc[i][j][r];
-        return;
-    }
-    store_tile<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, y, m0 + BM <= Cout && n0 + BNT <= N);
+    store_tile<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, y, m0 + BM <= Cout && n0 + BNT <= N, inv);
 }
 
 // ------------------------------------------------------------------ 3x3, input halo staged once per channel group
@@ -959,21 +762,11 @@ __global__ void __launch_bounds__(WS ? 2 * NT : NT, WS ? 1 : 2) conv_psa_kernel(
 // tap (a second barrier then), the partner workgroup's MFMAs covering that bubble.
 // BNT1: pixels per team tile — 256, or 192 for the 96-wide planes (two rows; 128-row
 // tiles only: wave tile 64 x 96, three 32-pixel fragments)
-// M16 (6xbf16, one halo buffer): the matrix work on v_mfma_f32_16x16x32_bf16 with the six
-// piece products paired along K — (hi.lo + lo.hi), (hi.mid + mid.hi), (mid.mid + hi.hi), the
-// A fragment [X | Y] and the B fragment [U | V] being pieces X, Y / U, V of the same 16
-// channels in the two k halves — so three 32-k MFMAs per 16 x 16 tile and K step, the same
-// MFMA cycles as six 32x32x16 per 32 x 32 tile.  The chip holds a higher clock on this shape
-// (the roofline kernel is DVFS-held: DESIGN §6 round 5); a 16 x 16 tile drains 4 adds.
-// PAIR (with M16, 64-row tiles): a K step is two taps of a channel group (the ninth alone), its
-// A image [piece][64 rows][64 B] holding both, so each 16x16 tile's chain is six MFMAs over 32
-// channels x 2 taps and drains once per two taps (half the adds); waves 32 rows x 128 pixels.
-template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2, int BNT1 = 256, bool M16 = false, bool PAIR = false>
+template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2, int BNT1 = 256>
 __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
-                                                        int B, int Cin, int H, int Cout) {
-    UBPL_STAMP_BEGIN
+                                                        int B, int Cin, int H, int Cout, float osc) {
     constexpr int BNT = BNT1 * TEAMS, R = BNT / WW, W2 = WW + 2;
     static_assert(BNT1 == 256 || (BNT1 == 192 && BM == 128), "192-pixel tiles: 128 rows");
     constexpr int NW = 4 * TEAMS;              // waves (TEAMS 4-wave teams, one 256-pixel tile each)
@@ -983,34 +776,24 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
                                                // piece starts at HPX - 32, rewriting pixels it overlaps)
     constexpr int HTOT = NP * HI;
     constexpr int NH = (HTOT + NW - 1) / NW;   // halo DMA instructions per wave (spares repeat the last one)
-    constexpr int AB = NP * BM * (PAIR ? 64 : 32);   // A bytes per K step
+    constexpr int AB = NP * BM * 32;           // A bytes per K step
     constexpr int AI = AB / 1024;              // A DMA instructions per K step (1 KB each)
-    constexpr int TPG = PAIR ? 5 : 9;          // K steps per channel group
     constexpr int NAW = (AI + NW - 1) / NW;    // per wave (spares repeat the last one)
     // GS (the one-piece path): a stage is a whole channel group — its halo and the
     // nine taps' A images (one barrier per 9 K steps; 8 MFMAs per wave per K step
     // left the per-step ring bound by its barriers); NS_G slots.  Otherwise A per
-    // K step in an NA-stage ring, halos double-buffered.
+    // K step in an NA-stage ring, halos double-buffered (NHB = 2) or one buffer
+    // reloaded at each group boundary (NHB = 1).
     constexpr bool GS = NP == 1;
     constexpr int NS_G = 3 * (NP * HB + 9 * AB) <= 160 * 1024 ? 3 : 2;
-    static_assert(NHB == 2 || (!GS && TEAMS == 1), "one halo buffer: 6xbf16, one team");
-    // NHB = 1: the next group's halo rows refilled as they fall out of use (row 0
-    // after the kh = 0 taps, row 1 after kh = 1; rows 2 .. R+1 at the group boundary,
-    // only rows 2 .. R-1 waited for there) with UBPL_PSAH_BAND=1 (build-time; slower);
-    // by default the whole halo is reloaded and waited for at each group boundary
-    constexpr bool HBAND = UBPL_PSAH_BAND != 0;
-#define BAND_W(NR_) ((NP * (((NR_) * W2 + 31) / 32) + NW - 1) / NW)
+    static_assert(NHB == 2 || (!GS && TEAMS == 1), "one halo buffer: split pieces, one team");
     // (one halo buffer: as many A stages, 2 .. UBPL_PSAH_NA_MAX, as fit two workgroups per CU)
     constexpr int NA1 = UBPL_PSAH_NA_MAX * AB + NP * HB <= 80 * 1024 ? UBPL_PSAH_NA_MAX
                         : (3 * AB + NP * HB <= 80 * 1024 ? 3 : 2);
     constexpr int NA = GS ? 9 * NS_G : (NHB == 1 ? NA1 : 3);   // A images
-    constexpr int WROWS = PAIR ? 32 : 64;      // rows of a wave tile
-    constexpr int WGM = BM / WROWS, WGN = 4 / WGM;
+    constexpr int WGM = BM / 64, WGN = 4 / WGM;
     constexpr int TM = 2, TN = BNT1 / WGN / 32;
-    constexpr int TM16 = WROWS / 16, TN16 = BNT1 / WGN / 16;   // M16: 16 x 16 blocks of the wave tile
     static_assert(BM == 64 || BM == 128, "64- or 128-row tiles");
-    static_assert(!M16 || (NP == 3 && TEAMS == 1 && NHB == 1), "M16: 6xbf16, one halo buffer");
-    static_assert(!PAIR || (M16 && BM == 64 && !UBPL_PSAH_BAND), "PAIR: M16, 64-row tiles");
     constexpr int OFF_H = NA * AB, LDS_BYTES = OFF_H + (GS ? NS_G : NHB) * NP * HB;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS");
     static_assert(BNT % WW == 0 && WW % 32 == 0, "whole rows of 32-pixel fragments");
@@ -1021,7 +804,7 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
     const int Ktot = Cin * 9;
     // (wid wave-uniform in an SGPR: the DMA index math below stays scalar)
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = ((wid & 3) / WGN) * WROWS, wn = (wid >> 2) * BNT1 + ((wid & 3) % WGN) * (BNT1 / WGN);
+    const int wm = ((wid & 3) / WGN) * 64, wn = (wid >> 2) * BNT1 + ((wid & 3) % WGN) * (BNT1 / WGN);
     const int lam = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int by = lam % gridDim.y, bx = lam / gridDim.y;
     const int m0 = by * BM;
@@ -1048,29 +831,6 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
                                              (lds_ptr_t)dst, 16, 0, 0);
         }
     };
-    // PAIR: the A image of K step s = taps (2j, 2j+1) of group cg (j = 4: tap 8, its 32 B
-    // loaded twice): row r's four 16-B chunks (c = 2 tap + half) at position c ^ ((r >> 2) & 3),
-    // 16 rows per instruction (lane: row lane / 4, position lane % 4)
-    auto stage_a2 = [&](int slot, int s) {
-        const int cg = s / TPG, j = s - cg * TPG;
-        const int k0 = cg * 144 + j * 32;
-        const int rl = lane >> 2, pos = lane & 3;
-#pragma unroll
-        for (int u = 0; u < NAW; ++u) {
-            const int i = min(u * NW + wid, AI - 1);   // (a spare repeats the last: same bytes)
-            const int p = i / (BM / 16), rb = i % (BM / 16);
-            const int row = 16 * rb + rl;
-            const int csrc = pos ^ ((row >> 2) & 3);
-            const int kk = k0 + 8 * (j == 4 ? (csrc & 1) : csrc);
-            const uint16_t* src = wp + (int64_t)p * wplane + (int64_t)min(m0 + row, Cout - 1) * Ktot + kk;
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(lds + slot * AB + p * BM * 64 + rb * 1024),
-                                             16, 0, 0);
-        }
-    };
-    auto stage_A = [&](int slot, int s) {
-        if constexpr (PAIR) stage_a2(slot, s);
-        else stage_a(slot, s);
-    };
     // halo of group cg: instruction i = wid * NH + u (piece i / HI, 32-pixel chunk i % HI)
     auto stage_h = [&](int buf, int cg) {
         const int64_t gpx = (((int64_t)b * G + cg) * Hp + oh0) * W2;   // first halo pixel (PSA pixel index)
@@ -1083,29 +843,10 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             const int i = min(wid * NH + u, HTOT - 1);  // (a spare repeats the last: same bytes)
             const int p = i / HI, c0 = min((i - p * HI) * 32, HPX - 32);
             const int q = c0 + lr;
-            const int ch = M16 ? lo : lo ^ ((q >> 3) & 1);   // (M16: unswizzled, see step16)
+            const int ch = lo ^ ((q >> 3) & 1);
             const char* src = reinterpret_cast<const char*>(xs + p * xplane + (gpx + q) * 16) + ch * 16;
             char* dst = lds + OFF_H + (buf * NP + p) * HB + c0 * 32;
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)dst, 16, 0, 0);
-        }
-    };
-    // halo rows [R0, R0 + NR) of group cg into the one buffer (NHB = 1): the band's
-    // pixels only (its last chunk starts 32 pixels before the band's end), BAND_W(NR)
-    // instructions per wave
-    auto stage_band = [&](auto r0c, auto nrc, int cg) {
-        constexpr int R0 = decltype(r0c)::value, NR = decltype(nrc)::value;
-        constexpr int BPX = NR * W2, BI = (BPX + 31) / 32, BT = NP * BI, BW = (BT + NW - 1) / NW;
-        const int64_t gpx = (((int64_t)b * G + cg) * Hp + oh0) * W2;
-        int lr = lane >> 1, lo = lane & 1;
-        asm volatile("" : "+v"(lr), "+v"(lo));
-#pragma unroll
-        for (int u = 0; u < BW; ++u) {
-            const int i = min(wid * BW + u, BT - 1);
-            const int p = i / BI, c0 = R0 * W2 + min((i - p * BI) * 32, BPX - 32);
-            const int q = c0 + lr;
-            const int ch = M16 ? lo : lo ^ ((q >> 3) & 1);
-            const char* src = reinterpret_cast<const char*>(xs + p * xplane + (gpx + q) * 16) + ch * 16;
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(lds + OFF_H + p * HB + c0 * 32), 16, 0, 0);
         }
     };
 
@@ -1125,200 +866,17 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
     };
     // halo pixel of tap (0, 0) for tile-local output pixel nt: row nt / WW, column nt % WW
     const int nt0 = wn + li;
-    floatx16 acc[TM][TN];   // (dead with M16)
-    // M16: lane (c16 = lane % 16, kc = lane / 16): fragment row / column c16, k chunk kc (8
-    // channels: chunk kc & 1 of piece X (kc < 2) or Y); output rows 4 kc + r of column c16
-    const int c16 = lane & 15, kc = lane >> 4;
-    floatx4 acc4[M16 ? TM16 : 1][M16 ? TN16 : 1];
-    auto out_base16 = [&](int j, int64_t& ob, bool& ok) {
-        const int64_t n = n0 + wn + 16 * j + c16;
-        ok = n < N;
-        const int64_t nc = ok ? n : N - 1;
-        const int bb = (int)(nc / P);
-        ob = (int64_t)bb * Cout * P + (nc - (int64_t)bb * P);
-    };
-    if constexpr (M16) {
-#pragma unroll
-        for (int j = 0; j < TN16; ++j) {
-            int64_t ob;
-            bool ok;
-            out_base16(j, ob, ok);
-#pragma unroll
-            for (int i = 0; i < TM16; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int m = min(m0 + wm + 16 * i + 4 * kc + r, Cout - 1);
-                    float v = bias != nullptr ? bias[m] : 0.f;
-                    if (res != nullptr) v += res[ob + (int64_t)m * P];
-                    acc4[i][j][r] = v;
-                }
-        }
-    } else {
+    floatx16 acc[TM][TN];
+    {
         int64_t obase[TN];
         bool nok[TN];
         out_base(obase, nok);
-        ubpl::seed_acc<TM, TN, true>(acc, bias, res, obase, m0 + wm, Cout, P);
+        ubpl::seed_acc<TM, TN, true>(acc, bias, res, obase, m0 + wm, Cout, P, osc);
     }
 
     // one K step (group cg's tap at pixel offset toff): fragments from the A image
     // at abase and the halo image at hbase
-    // M16 K step: A fragments of the four row blocks ([hi|lo], [hi|mid], [mid|hi]); per 16-pixel
-    // block the B fragments [lo|hi], [mid|hi] (read one block ahead); per tile the chain
-    // (hi.lo + lo.hi) -> (hi.mid + mid.hi) -> (mid.mid + hi.hi) from zero, drained with 4 adds
-    // (M16) per-lane byte offsets of the B rows at tap (0, 0), one per 16-pixel block: the
-    // halo is unswizzled for this kernel (16 consecutive pixels per read group: no bank
-    // conflict), so a K step adds only its uniform tap offset
-    uint32_t boff[M16 ? TN16 : 1];
-    if constexpr (M16) {
-#pragma unroll
-        for (int j = 0; j < TN16; ++j) {
-            const int nt = wn + 16 * j + c16;
-            boff[j] = (uint32_t)((nt + (nt / WW) * 2) * 32 + 16 * (kc & 1));
-        }
-    }
-    auto step16 = [&](const char* abase, const char* hbase, int toff) {
-        const int ch = kc & 1, yh = kc >> 1;
-        bf16x8 a1[TM16], a2[TM16], a3[TM16];
-#pragma unroll
-        for (int i = 0; i < TM16; ++i) {
-            const int row = wm + 16 * i + c16;
-            const char* ar = abase + row * 32 + 16 * (ch ^ ((row >> 3) & 1));
-            a1[i] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 2 : 0) * BM * 32);
-            a2[i] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 1 : 0) * BM * 32);
-            a3[i] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 0 : 1) * BM * 32);
-        }
-        const char* hb_t = hbase + toff * 32;
-        auto read_b16 = [&](int j, bf16x8& b1, bf16x8& b2) {
-            const char* br = hb_t + boff[j];
-            b1 = *reinterpret_cast<const bf16x8*>(br + (yh ? 0 : 2) * HB);
-            b2 = *reinterpret_cast<const bf16x8*>(br + (yh ? 0 : 1) * HB);
-        };
-        bf16x8 b1, b2, n1, n2;
-        read_b16(0, b1, b2);
-        const floatx4 zero = {};
-        // ping-pong: tile q's chain issued with tile q-1's four drain adds in its gaps
-        floatx4 prev;
-#pragma unroll
-        for (int q = 0; q < TM16 * TN16; ++q) {
-            const int j = q / TM16, i = q % TM16;
-            if (i == 0 && j > 0) {
-                b1 = n1;
-                b2 = n2;
-            }
-            floatx4 cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1, zero, 0, 0, 0);
-            cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[i], b2, cur, 0, 0, 0);
-            cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[i], b2, cur, 0, 0, 0);
-            const bool pf = i == 0 && j + 1 < TN16;
-            if (pf) read_b16(j + 1, n1, n2);
-            if (q > 0) {
-                const int pj = (q - 1) / TM16, pi = (q - 1) % TM16;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float v = acc4[pi][pj][r] + prev[r];
-                    asm("" : "+v"(v));
-                    acc4[pi][pj][r] = v;
-                }
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-                if (pf) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            prev = cur;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float v = acc4[TM16 - 1][TN16 - 1][r] + prev[r];
-            asm("" : "+v"(v));
-            acc4[TM16 - 1][TN16 - 1][r] = v;
-        }
-    };
-    // PAIR K step: taps a (halo offset ta) and, when TWO, b (tb); per tile the chain
-    // P1a P1b P2a P2b P3a P3b from zero (P1 = hi.lo + lo.hi, P2 = hi.mid + mid.hi,
-    // P3 = mid.mid + hi.hi), one 4-add drain
-    auto step16p = [&](auto twoc, const char* abase, const char* hbase, int ta, int tb) {
-        constexpr bool TWO = decltype(twoc)::value;
-        constexpr int NT2 = TWO ? 2 : 1;
-        const int ch = kc & 1, yh = kc >> 1;
-        bf16x8 af[NT2][TM16][3];
-#pragma unroll
-        for (int i = 0; i < TM16; ++i) {
-            const int row = wm + 16 * i + c16;
-#pragma unroll
-            for (int h2 = 0; h2 < NT2; ++h2) {
-                const char* ar = abase + row * 64 + 16 * ((2 * h2 + ch) ^ ((row >> 2) & 3));
-                af[h2][i][0] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 2 : 0) * BM * 64);
-                af[h2][i][1] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 1 : 0) * BM * 64);
-                af[h2][i][2] = *reinterpret_cast<const bf16x8*>(ar + (yh ? 0 : 1) * BM * 64);
-            }
-        }
-        const char* hb_a = hbase + ta * 32;
-        const char* hb_b = hbase + tb * 32;
-        auto read_b = [&](int j, bf16x8 (&bo)[NT2][2]) {
-#pragma unroll
-            for (int h2 = 0; h2 < NT2; ++h2) {
-                const char* br = (h2 ? hb_b : hb_a) + boff[j];
-                bo[h2][0] = *reinterpret_cast<const bf16x8*>(br + (yh ? 0 : 2) * HB);
-                bo[h2][1] = *reinterpret_cast<const bf16x8*>(br + (yh ? 0 : 1) * HB);
-            }
-        };
-        bf16x8 bc[NT2][2], bn[NT2][2];
-        read_b(0, bc);
-        const floatx4 zero = {};
-        floatx4 prev;
-#pragma unroll
-        for (int q = 0; q < TM16 * TN16; ++q) {
-            const int j = q / TM16, i = q % TM16;
-            if (i == 0 && j > 0) {
-#pragma unroll
-                for (int h2 = 0; h2 < NT2; ++h2) {
-                    bc[h2][0] = bn[h2][0];
-                    bc[h2][1] = bn[h2][1];
-                }
-            }
-            floatx4 cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i][0], bc[0][0], zero, 0, 0, 0);
-            if constexpr (TWO) cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i][0], bc[1][0], cur, 0, 0, 0);
-            cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i][1], bc[0][1], cur, 0, 0, 0);
-            if constexpr (TWO) cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i][1], bc[1][1], cur, 0, 0, 0);
-            cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i][2], bc[0][1], cur, 0, 0, 0);
-            if constexpr (TWO) cur = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i][2], bc[1][1], cur, 0, 0, 0);
-            const bool pf = i == 0 && j + 1 < TN16;
-            if (pf) read_b(j + 1, bn);
-            if (q > 0) {
-                const int pj = (q - 1) / TM16, pi = (q - 1) % TM16;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float v = acc4[pi][pj][r] + prev[r];
-                    asm("" : "+v"(v));
-                    acc4[pi][pj][r] = v;
-                }
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-                if (pf) __builtin_amdgcn_sched_group_barrier(0x100, 2 * NT2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-                if constexpr (TWO) __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            prev = cur;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float v = acc4[TM16 - 1][TN16 - 1][r] + prev[r];
-            asm("" : "+v"(v));
-            acc4[TM16 - 1][TN16 - 1][r] = v;
-        }
-    };
     auto step = [&](const char* abase, const char* hbase, int toff) {
-        if constexpr (M16) {
-            step16(abase, hbase, toff);
-        } else {
         bf16x8 af[TM][NP], bfr[TN][NP];
         auto read_b = [&](int j) {
             const int nt = nt0 + 32 * j;
@@ -1356,16 +914,10 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
                 const int j = q / TM, i = q % TM, pj = (q - 1) / TM, pi = (q - 1) % TM;
                 const floatx16 cur = mfma_split0<NP>(af[i], bfr[j]);
                 drain(acc[pi][pj], prev);
-#pragma unroll
-                for (int g = 0; g < 6; ++g) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
+                pp_schedule<NP>();
                 prev = cur;
             }
             drain(acc[TM - 1][TN - 1], prev);
-        }
         }
     };
 
@@ -1395,37 +947,12 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
     } else {
-        const int nk = G * TPG;
+        const int nk = G * 9;
         stage_h(0, 0);
-        for (int a = 0; a < NA - 1 && a < nk; ++a) stage_A(a, a);
-        const bool younger = (blockIdx.x + gridDim.x * blockIdx.y) >= (gridDim.x * gridDim.y) / 2;
+        for (int a = 0; a < NA - 1 && a < nk; ++a) stage_a(a, a);
         for (int s = 0; s < nk; ++s) {
-            fair_prio<8>(s, younger);
-            const int cg = s / TPG, tap = s - cg * TPG;   // (PAIR: tap = the pair index)
-            if (NHB == 1 && HBAND && tap == 0 && cg > 0) {
-                // every wave done with group cg - 1: halo rows 2 .. R-1 (rows 0 and 1 came
-                // in at taps 3 and 6 of the previous group) now, waited for; rows R, R+1
-                // (first read at taps 3 and 6) behind them, left in flight
-                vm_wait<(NA - 2) * NAW>();
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-                if constexpr (R > 2) {
-                    stage_band(std::integral_constant<int, 2>{}, std::integral_constant<int, R - 2>{}, cg);
-                    vm_wait<0>();
-                }
-            } else if (NHB == 1 && HBAND) {
-                // A(s) landed; younger than it and allowed in flight: the NA - 2 A images
-                // after it, and a halo band issued after it (one issued at step u follows
-                // A(u + NA - 1): younger when s - u is 1 .. NA - 1; rows R, R+1 at tap 0,
-                // row 0 at tap 3, row 1 at tap 6)
-                const bool nxt = cg + 1 < G;
-                const int d3 = tap - 3, d6 = tap - 6;
-                if (s + 1 >= nk) vm_wait<0>();
-                else if (tap >= 1 && tap <= NA - 1 && cg > 0) vm_wait<(NA - 2) * NAW + BAND_W(2)>();
-                else if (((d3 >= 1 && d3 <= NA - 1) || (d6 >= 1 && d6 <= NA - 1)) && nxt)
-                    vm_wait<(NA - 2) * NAW + BAND_W(1)>();
-                else vm_wait<(NA - 2) * NAW>();
-            } else if (NHB == 1 && tap == 0 && cg > 0 && !UBPL_PSAH_NORELOAD) {
+            const int cg = s / 9, tap = s - cg * 9;
+            if (NHB == 1 && tap == 0 && cg > 0) {
                 // every wave done with group cg - 1: reload the one halo buffer, wait for it
                 vm_wait<(NA - 2) * NAW>();
                 __builtin_amdgcn_s_barrier();
@@ -1435,10 +962,9 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             } else if (NHB == 1) {
                 if (s + 1 < nk) vm_wait<(NA - 2) * NAW>();
                 else vm_wait<0>();
-            } else
-            // A(s) and (tap 0) halo(cg) landed; the A images issued after A(s) (NA - 2
-            // of them) and the next group's halo, when issued after A(s), may stay in flight
-            if (s + 1 < nk) {
+            } else if (s + 1 < nk) {
+                // A(s) and (tap 0) halo(cg) landed; the A images issued after A(s) (NA - 2
+                // of them) and the next group's halo, when issued after A(s), may stay in flight
                 if (tap >= 1 && tap <= NA - 1 && cg + 1 < G) vm_wait<(NA - 2) * NAW + NH>();
                 else vm_wait<(NA - 2) * NAW>();
             } else {
@@ -1446,56 +972,18 @@ __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel
             }
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            if (s + NA - 1 < nk) stage_A((s + NA - 1) % NA, s + NA - 1);
+            if (s + NA - 1 < nk) stage_a((s + NA - 1) % NA, s + NA - 1);
             if (NHB == 2 && tap == 0 && cg + 1 < G) stage_h((cg + 1) & 1, cg + 1);
-            if constexpr (NHB == 1 && HBAND) {
-                if (tap == 0 && cg > 0)
-                    stage_band(std::integral_constant<int, R>{}, std::integral_constant<int, 2>{}, cg);
-                if (tap == 3 && cg + 1 < G)
-                    stage_band(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}, cg + 1);
-                if (tap == 6 && cg + 1 < G)
-                    stage_band(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, cg + 1);
-            }
-            if constexpr (PAIR) {
-                const int t0 = 2 * tap, t1 = t0 + 1;
-                const int off0 = (t0 / 3) * W2 + t0 % 3, off1 = (t1 / 3) * W2 + t1 % 3;
-                if (tap < 4) step16p(std::true_type{}, lds + (s % NA) * AB, lds + OFF_H, off0, off1);
-                else step16p(std::false_type{}, lds + (s % NA) * AB, lds + OFF_H, off0, off0);
-            } else {
-                const int kh = tap / 3;
-                step(lds + (s % NA) * AB, lds + OFF_H + (NHB == 2 ? (cg & 1) : 0) * NP * HB, kh * W2 + (tap - 3 * kh));
-            }
+            const int kh = tap / 3;
+            step(lds + (s % NA) * AB, lds + OFF_H + (NHB == 2 ? (cg & 1) : 0) * NP * HB, kh * W2 + (tap - 3 * kh));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
     }
-    UBPL_STAMP_END
 
-    if constexpr (M16) {
-#pragma unroll
-        for (int j = 0; j < TN16; ++j) {
-            int64_t ob;
-            bool ok;
-            out_base16(j, ob, ok);
-            if (!ok) continue;
-#pragma unroll
-            for (int i = 0; i < TM16; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int m = m0 + wm + 16 * i + 4 * kc + r;
-                    if (m < Cout) {
-                        float* d = y + ob + (int64_t)m * P;
-                        if (UBPL_NT_EPI) __builtin_nontemporal_store(acc4[i][j][r], d);
-                        else *d = acc4[i][j][r];
-                    }
-                }
-        }
-    } else {
-        int64_t obase[TN];
-        bool nok[TN];
-        out_base(obase, nok);
-        store_tile<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, y, m0 + BM <= Cout && n0 + BNT <= N);
-    }
-    UBPL_STAMP_EXIT
+    int64_t obase[TN];
+    bool nok[TN];
+    out_base(obase, nok);
+    store_tile<TM, TN>(acc, nok, obase, m0 + wm, Cout, P, y, m0 + BM <= Cout && n0 + BNT <= N, 1.f / osc);
 }
 
 // ------------------------------------------------------------------ 1x1, split on load
@@ -1521,13 +1009,14 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
                                                            const float* __restrict__ pscale,
                                                            const float* __restrict__ pshift, const float* res,
                                                            float* y, int B, int K, int P, int M,
-                                                           float* __restrict__ stat_part, ubpl::BnBwdEpi bwd) {
-    // NP = 3: 6xbf16 (f32-equivalent); NP = 1: the "bf16" precision (operands
-    // rounded to bf16, one MFMA per product, accumulated in f32 directly)
+                                                           float* __restrict__ stat_part, ubpl::BnBwdEpi bwd,
+                                                           float asc, float osc) {
+    // NP = 3: 6xbf16 (f32-equivalent); NP = 2: 2xfp16 (activations scaled by asc after the
+    // prologue, accumulators by osc = weight scale x asc, undone at the stores); NP = 1: the
+    // "bf16" precision (operands rounded to bf16, one MFMA per product, accumulated in f32)
     // NS: stages in the LDS ring (2, or 3 with 64-row tiles: two K steps' DMA in flight);
     // NSB = 3 with NS = 2: a deeper ring for the activation stream alone (HBM: two K
     // steps of it in flight per workgroup) beside the weights' two stages (L2-resident)
-    UBPL_STAMP_BEGIN
     static_assert(BNT == 256 || BNT == 128, "256- or 128-pixel tiles");
     static_assert(NSB == NS || (NS == 2 && NSB == 3), "B ring: as deep as A's, or 3 beside A's 2");
     constexpr int TM = BM / 32, TN = BNT / 128;
@@ -1544,7 +1033,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     const int64_t N = (int64_t)B * P;
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // (wave-uniform: SGPR)
     const int wn = (BNT / 4) * wid;
-    if (PRO && UBPL_SOL_LDS_COEF) {
+    if (PRO) {
         for (int k = tid; k < K; k += NT) {
             lds_sc[k] = pscale[k];
             lds_sh[k] = pshift[k];
@@ -1563,10 +1052,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     const int lr = lane >> 1;
     const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
     const bool a_issue = BM / 32 >= NT / 64 || wid < BM / 32;   // every wave when BM >= 128
-    // (UBPL_SOL_ACONTIG, timing-only diagnostic: the weight DMA reads one contiguous KB per
-    // instruction instead of 32 rows' 32 B — wrong results)
-    const uint32_t a_lane = UBPL_SOL_ACONTIG ? (uint32_t)((32 * wid + lr) * 32 + 16 * lchunk)
-                                             : (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, M - 1) * K + 8 * lchunk) * 2);
+    const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * wid + lr, M - 1) * K + 8 * lchunk) * 2);
     // B DMA: wave w moves k rows 4w..4w+3; 256-pixel tiles: one row per instruction,
     // lane L pixels n0 + 4L .. +3; 128-pixel tiles: two rows per instruction, lanes
     // 32-63 the second (P % 4 == 0)
@@ -1580,7 +1066,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     }
     auto stage_a = [&](int buf, int kt) {
         char* base = lds + buf * AB;
-        if (a_issue && UBPL_SOL_NODMA != 1 && UBPL_SOL_NODMA != 2) {
+        if (a_issue) {
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
                 const char* ab = reinterpret_cast<const char*>(wp + p * wplane + kt);
@@ -1591,9 +1077,8 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     };
     auto stage_b = [&](int buf, int kt) {
         char* base = lds + NS * AB + buf * BB;
-        if (UBPL_SOL_NODMA == 1) return;
 #pragma unroll
-        for (int q = 0; q < (UBPL_SOL_NODMA == 3 ? BQ / 2 : BQ); ++q) {
+        for (int q = 0; q < BQ; ++q) {
             const int r = 4 * wid + q * (4 / BQ);
             const char* bb = reinterpret_cast<const char*>(x + (int64_t)(kt + r) * P);
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
@@ -1632,21 +1117,14 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     // without a residual the scalar epilogue measured faster
     const bool tepi = UBPL_SOL_TEPI && BNT == 256 && !EPI && res != nullptr &&
                       ((((uintptr_t)y) | (uintptr_t)res) & 15) == 0;
-    ubpl::seed_acc<TM, TN>(acc, bias, tepi ? nullptr : res, obase, m0, M, P);
+    ubpl::seed_acc<TM, TN>(acc, bias, tepi ? nullptr : res, obase, m0, M, P, osc);
+    const float inv = 1.f / osc;
 
     const int nkt = K >> 4;
     constexpr bool deepb = NSB != NS;
     // this lane's k half of K step kt: 8 (scale, shift) pairs of the prologue
     auto load_coef = [&](int kt, float (&sc)[8], float (&sh)[8]) {
-        if (PRO && !UBPL_SOL_LDS_COEF) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float s0 = pscale[kt + e], s1 = pscale[kt + 8 + e];
-                const float h0 = pshift[kt + e], h1 = pshift[kt + 8 + e];
-                sc[e] = h ? s1 : s0;
-                sh[e] = h ? h1 : h0;
-            }
-        } else if (PRO) {
+        if (PRO) {
             const float4* qs = reinterpret_cast<const float4*>(lds_sc + kt + 8 * h);
             const float4* qh = reinterpret_cast<const float4*>(lds_sh + kt + 8 * h);
             const float4 s0 = qs[0], s1 = qs[1], h0 = qh[0], h1 = qh[1];
@@ -1665,14 +1143,13 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         for (int e = 0; e < 8; ++e) {
             v[e] = bs[e * BNT + 32 * j];
             if (PRO) v[e] = fmaxf(fmaf(v[e], sc[e], sh[e]), 0.f);
+            if constexpr (NP == 2) v[e] *= asc;
         }
         uint32_t pk[NP][4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             uint32_t o[NP];
-            if (UBPL_SOL_NOSPLIT) split2<1>(v[2 * e], v[2 * e + 1], *reinterpret_cast<uint32_t(*)[1]>(o));
-            if (UBPL_SOL_NOSPLIT) for (int p = 1; p < NP; ++p) o[p] = o[0] ^ (uint32_t)p;
-            else split2<NP>(v[2 * e], v[2 * e + 1], o);
+            split2<NP>(v[2 * e], v[2 * e + 1], o);
 #pragma unroll
             for (int p = 0; p < NP; ++p) pk[p][e] = o[p];
         }
@@ -1685,13 +1162,7 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
     stage(0, 0);
     if (NS == 3 && nkt > 1) stage(1, 16);
     if (deepb && nkt > 1) stage_b(1, 16);
-    const bool younger = (blockIdx.x + gridDim.x * blockIdx.y) >= (gridDim.x * gridDim.y) / 2;
-#if UBPL_CLOCK_STAMP == 3
-    unsigned long long ph[4] = {0, 0, 0, 0};
-#endif
     for (int t = 0; t < nkt; ++t) {
-        UBPL_PH(p0)
-        fair_prio<2>(t, younger);
         // stage t landed for every wave (NS = 3: this wave's stage t+1 DMA may stay in
         // flight; deepb: B(t+1), issued after A(t), may stay in flight), every wave
         // done with stage t-1
@@ -1705,7 +1176,6 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        UBPL_PH(p1)
         if (deepb) {
             // A(t+1) first, then B(t+2): the next wait leaves only B(t+2) in flight
             if (t + 1 < nkt) stage_a((t + 1) % NS, (t + 1) * 16);
@@ -1713,8 +1183,6 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         } else if (t + NS - 1 < nkt) {
             stage((t + NS - 1) % NS, (t + NS - 1) * 16);
         }
-        UBPL_PH(p2)
-        if (UBPL_SOL_NOCOMP) continue;
         const int kt = t * 16;
         const char* base = lds + (t % NS) * AB;                       // A of stage t
         const char* bbase = lds + NS * AB + (t % NSB) * BB;           // B of stage t
@@ -1723,7 +1191,6 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
         bf16x8 bfr[TN][NP];
 #pragma unroll
         for (int j = 0; j < TN; ++j) split_col(bbase, j, sc, sh, bfr[j]);
-        UBPL_PH(p3)
         if constexpr (NP == 1) {
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
@@ -1740,83 +1207,18 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
             for (int p = 0; p < NP; ++p)
                 o[p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
         };
-#if UBPL_SOL_PP
-        // ping-pong chunks (as conv_psa_kernel): tile (i, j)'s chain is issued with the
-        // previous tile's drain adds between its MFMAs, and row block i+1's A fragments
-        // are read during row block i (one continuous MFMA stream over the K step)
-        floatx16 prev;
-        bf16x8 afc[NP], afn[NP];
-        lda(0, afc);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const floatx16 cur = mfma_split0<NP>(afc, bfr[j]);
-                const bool pf = j == 0 && i + 1 < TM;
-                if (pf) lda(i + 1, afn);
-                if (i + j > 0) {
-                    const int q = i * TN + j - 1;
-                    drain(acc[q / TN][q % TN], prev);
-                    // the prefetch after the chain's first MFMA: the wait the compiler puts
-                    // before that MFMA (for this row's fragments) then covers no new read
-#pragma unroll
-                    for (int g = 0; g < 6; ++g) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                        if (g == 0 && pf) __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                prev = cur;
-            }
-            if (i + 1 < TM) {
-#pragma unroll
-                for (int p = 0; p < NP; ++p) afc[p] = afn[p];
-            }
-        }
-        drain(acc[TM - 1][TN - 1], prev);
-#else
-        bf16x8 afn[NP];
-        if (UBPL_SOL_APF == 2) lda(0, afn);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             bf16x8 af[NP];
-            if (UBPL_SOL_APF == 2) {
-                // row block i+1's A fragments read ahead of row block i's MFMAs
+            lda(i, af);
 #pragma unroll
-                for (int p = 0; p < NP; ++p) af[p] = afn[p];
-                if (i + 1 < TM) lda(i + 1, afn);
-            } else {
-                lda(i, af);
-            }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                // per-chunk accumulation (see conv_fwd_split_kernel)
-                if (UBPL_SOL_NOCHUNK) mfma_split<NP>(acc[i][j], af, bfr[j]);
-                else drain(acc[i][j], mfma_split0<NP>(af, bfr[j]));
-            }
+            for (int j = 0; j < TN; ++j) drain(acc[i][j], mfma_split0<NP>(af, bfr[j]));   // per-chunk accumulation
             // (register budget: one row block's A fragments live at a time)
-            if (UBPL_SOL_APF != 1) __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_sched_barrier(0);
         }
-#endif
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#if UBPL_CLOCK_STAMP == 3
-        UBPL_PH(p4)
-        ph[0] += p1 - p0;
-        ph[1] += p2 - p1;
-        ph[2] += p3 - p2;
-        ph[3] += p4 - p3;
-#endif
     }
-#if UBPL_CLOCK_STAMP == 3
-    if (threadIdx.x == 0) {
-        const int sb = (blockIdx.x + gridDim.x * blockIdx.y) & 0xffff;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) g_clk_stamp[q][sb] = ph[q];
-    }
-#endif
-    UBPL_STAMP_END
 
     out_base(obase, nok);
     if constexpr (EPI) {
@@ -1856,313 +1258,15 @@ __global__ void __launch_bounds__(NT, BNT == 128 ? 3 : UBPL_SOL_LB) conv1x1_sol_
                 const int m = m0 + 32 * i + row;
                 float4 v = *reinterpret_cast<const float4*>(img + row * RS + c4);
                 if (ok && m < M) {
-                    v.x += q[k].x; v.y += q[k].y; v.z += q[k].z; v.w += q[k].w;
+                    v.x = fmaf(v.x, inv, q[k].x); v.y = fmaf(v.y, inv, q[k].y);
+                    v.z = fmaf(v.z, inv, q[k].z); v.w = fmaf(v.w, inv, q[k].w);
                     *reinterpret_cast<float4*>(y + ob + (int64_t)m * P) = v;
                 }
             }
         }
         return;
     }
-    if (UBPL_SOL_NOSTORE || UBPL_SOL_NT_STORE) {   // (diagnostics)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            if (!nok[j]) continue;
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (m < M && (!UBPL_SOL_NOSTORE || acc[i][j][r] == 1234.5f)) {
-                        if (UBPL_SOL_NT_STORE) __builtin_nontemporal_store(acc[i][j][r], y + obase[j] + (int64_t)m * P);
-                        else y[obase[j] + (int64_t)m * P] = acc[i][j][r];
-                    }
-                }
-        }
-        return;
-    }
-    store_tile<TM, TN>(acc, nok, obase, m0, M, P, y, m0 + BM <= M && n0 + BNT <= N);
-    UBPL_STAMP_EXIT
-}
-
-// ------------------------------------------------------------------ 1x1, split on load, warp-specialized (round 5)
-// conv1x1_sol_kernel's arithmetic (y = W v + bias (+ res), v = relu(x*pscale + pshift)
-// or x, NP bf16 pieces per operand, 16-k chunks drained into f32 accumulators) with the
-// split taken off the MFMA waves: 512 threads, 4 MFMA waves (wave w: all 128 rows x
-// pixels 64w..64w+63 of the 256-pixel tile, as conv1x1_sol_kernel) and 4 loader waves.
-// The loader waves stream the operands by LDS-DMA — weights [piece][128 rows][32 B]
-// (3-slot ring, two K steps ahead), activations as f32 rows [16 k][256 px] (3-slot
-// ring, three K steps ahead) — and, one K step ahead of the MFMA waves, read the f32
-// image (thread = pixel: 16 ds_read_b32), apply the BN+ReLU prologue, split into NP
-// bf16 pieces and write them as the MFMA-ready image [piece][256 px][32 B] (chunk
-// swizzled by (px >> 3) & 1; 2-slot ring).  One s_barrier per K step for all eight
-// waves; a loader wave waits (counted vmcnt) for its own DMA of the next step's
-// operands before it.  The MFMA waves issue only fragment reads, MFMAs and the chunk
-// drains; the VALU of the split runs beside them on the loader waves of the same SIMD.
-// Persistent: one workgroup per CU walks tiles L, L + G, ... (L the XCD-remapped block
-// index), the step stream (tile, k) flattened, so the rings run across tile boundaries
-// and a tile's epilogue stores overlap the next tile's operand DMA.
-template <int NP, bool PRO>
-__global__ void __launch_bounds__(2 * NT, 1) conv1x1_ws_kernel(const float* __restrict__ x,
-                                                              const uint16_t* __restrict__ wp, int64_t wplane,
-                                                              const float* __restrict__ bias,
-                                                              const float* __restrict__ pscale,
-                                                              const float* __restrict__ pshift, const float* res,
-                                                              float* y, int B, int K, int P, int M, int ntiles) {
-    constexpr int BM = 128, BNT = 256, TM = 4, TN = 2;
-    constexpr int AB = NP * BM * 32;                // A stage: [piece][128 rows][32 B]
-    constexpr int BH = 8 * BNT * 4 + 128;           // f32 B stage half: 8 k rows (+ bank shift)
-    constexpr int BB = 2 * BH;
-    constexpr int PB = NP * BNT * 32;               // pieces stage: [piece][256 px][32 B]
-    constexpr int NSA = 3, NSB = 3, NSP = 2;
-    constexpr int OFF_B = NSA * AB, OFF_P = OFF_B + NSB * BB;
-    static_assert(OFF_P + NSP * PB <= 160 * 1024 - 2 * 4 * SOL_PRO_K, "LDS");
-    __shared__ __attribute__((aligned(16))) char lds[OFF_P + NSP * PB];
-    __shared__ __attribute__((aligned(16))) float lds_sc[PRO ? SOL_PRO_K : 4], lds_sh[PRO ? SOL_PRO_K : 4];
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool loader = wid >= 4;
-    const int lw = wid & 3;
-    if (PRO) {
-        for (int k = tid; k < K; k += 2 * NT) {
-            lds_sc[k] = pscale[k];
-            lds_sh[k] = pshift[k];
-        }
-        __syncthreads();
-    }
-    const int64_t N = (int64_t)B * P;
-    const int nkt = K >> 4;
-    const int gy = (M + BM - 1) / BM;
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int my_tiles = L < ntiles ? (ntiles - L + gridDim.x - 1) / gridDim.x : 0;
-    const int nsteps = my_tiles * nkt;
-    auto tile_of = [&](int s, int& m0, int64_t& n0) {
-        const int tl = L + (s / nkt) * gridDim.x;
-        m0 = (tl % gy) * BM;
-        n0 = (int64_t)(tl / gy) * BNT;
-    };
-
-    // ---- loader side: DMA and split
-    const int lr = lane >> 1;
-    const int lchunk = (lane & 1) ^ ((lr >> 3) & 1);
-    auto stage_a = [&](int s) {
-        int m0;
-        int64_t n0;
-        tile_of(s, m0, n0);
-        const int kt = (s % nkt) * 16;
-        const uint32_t a_lane = (uint32_t)(((int64_t)min(m0 + 32 * lw + lr, M - 1) * K + 8 * lchunk) * 2);
-        char* base = lds + (s % NSA) * AB;
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-            const char* ab = reinterpret_cast<const char*>(wp + p * wplane + kt);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(ab + a_lane), (lds_ptr_t)(base + p * BM * 32 + lw * 1024), 16,
-                                             0, 0);
-        }
-    };
-    auto stage_b = [&](int s) {
-        int m0;
-        int64_t n0;
-        tile_of(s, m0, n0);
-        const int kt = (s % nkt) * 16;
-        int64_t n = n0 + 4 * lane;
-        n = n < N ? n : N - 4;
-        const int64_t b = n / P;
-        const uint32_t b_lane = (uint32_t)((b * K * P + (n - b * P)) * 4);
-        char* base = lds + OFF_B + (s % NSB) * BB;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int r = 4 * lw + q;
-            const char* bb = reinterpret_cast<const char*>(x + (int64_t)(kt + r) * P);
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bb + b_lane),
-                                             (lds_ptr_t)(base + (r >> 3) * BH + (r & 7) * (BNT * 4)), 16, 0, 0);
-        }
-    };
-    // thread (tid - 256) = pixel px of the tile: 16 k values -> NP pieces, 2 x 16 B each
-    auto split_step = [&](int s) {
-        const int px = tid - 2 * 128;
-        const int kt = (s % nkt) * 16;
-        const float* bimg = reinterpret_cast<const float*>(lds + OFF_B + (s % NSB) * BB);
-        float v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = bimg[(k >> 3) * (BH / 4) + (k & 7) * BNT + px];
-        if (PRO) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = fmaxf(fmaf(v[k], lds_sc[kt + k], lds_sh[kt + k]), 0.f);
-        }
-        uint32_t pk[NP][8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            uint32_t o[NP];
-            split2<NP>(v[2 * e], v[2 * e + 1], o);
-#pragma unroll
-            for (int p = 0; p < NP; ++p) pk[p][e] = o[p];
-        }
-        char* pb = lds + OFF_P + (s % NSP) * PB + px * 32;
-        const int sw = (px >> 3) & 1;
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-            *reinterpret_cast<uint4*>(pb + p * (BNT * 32) + 16 * (0 ^ sw)) = make_uint4(pk[p][0], pk[p][1], pk[p][2], pk[p][3]);
-            *reinterpret_cast<uint4*>(pb + p * (BNT * 32) + 16 * (1 ^ sw)) = make_uint4(pk[p][4], pk[p][5], pk[p][6], pk[p][7]);
-        }
-    };
-    // this loader wave's outstanding DMA instructions allowed when A(s+1), B(s+2) must
-    // have landed: A(s+2) (NP) and B(s+3) (4), when issued
-    auto loader_wait = [&](int s) {
-        const bool a2 = s + 2 < nsteps, b3 = s + 3 < nsteps;
-        if (a2 && b3) vm_wait<NP + 4>();
-        else if (a2) vm_wait<NP>();
-        else vm_wait<0>();
-    };
-
-    if (loader) {
-        // prologue: A(0), B(0), A(1), B(1), B(2); then A(0), B(0) landed
-        if (nsteps > 0) { stage_a(0); stage_b(0); }
-        if (nsteps > 1) { stage_a(1); stage_b(1); }
-        if (nsteps > 2) stage_b(2);
-        if (nsteps > 2) vm_wait<NP + 8>();
-        else if (nsteps > 1) vm_wait<NP + 4>();
-        else vm_wait<0>();
-        __builtin_amdgcn_s_barrier();      // every loader's part of B(0) landed
-        asm volatile("" ::: "memory");
-        if (nsteps > 0) {
-            split_step(0);
-            // before barrier(0): B(1) landed (A(1) with it; B(2) may stay in flight)
-            if (nsteps > 2) vm_wait<4>();
-            else vm_wait<0>();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        for (int s = 0; s < nsteps; ++s) {
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            if (s + 2 < nsteps) stage_a(s + 2);
-            if (s + 3 < nsteps) stage_b(s + 3);
-            if (s + 1 < nsteps) split_step(s + 1);
-            loader_wait(s);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        return;
-    }
-
-    // ---- MFMA waves (the same barriers, one per step): per tile, seed / K loop / epilogue
-    const int li = lane & 31, h = lane >> 5;
-    const int wn = 64 * lw;
-    __builtin_amdgcn_s_barrier();          // the prologue barrier
-    asm volatile("" ::: "memory");
-    for (int it = 0; it < my_tiles; ++it) {
-        int m0;
-        int64_t n0;
-        tile_of(it * nkt, m0, n0);
-        floatx16 acc[TM][TN];
-        if (bias != nullptr) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float bv = bias[min(m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1)];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[i][j][r] = bv;
-                }
-        } else {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-        }
-        for (int t = 0; t < nkt; ++t) {
-            const int s = it * nkt + t;
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            const char* abase = lds + (s % NSA) * AB;
-            const char* pbase = lds + OFF_P + (s % NSP) * PB;
-            auto read_b = [&](int j, bf16x8 (&bf)[NP]) {
-                const int px = wn + 32 * j + li;
-#pragma unroll
-                for (int p = 0; p < NP; ++p)
-                    bf[p] = *reinterpret_cast<const bf16x8*>(pbase + p * (BNT * 32) + px * 32 +
-                                                             16 * (h ^ ((px >> 3) & 1)));
-            };
-            auto read_a = [&](int i, bf16x8 (&af)[NP]) {
-                const int row = 32 * i + li;
-#pragma unroll
-                for (int p = 0; p < NP; ++p)
-                    af[p] = *reinterpret_cast<const bf16x8*>(abase + p * BM * 32 + row * 32 +
-                                                             16 * (h ^ ((row >> 3) & 1)));
-            };
-            if constexpr (NP == 1) {
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    bf16x8 bf[NP];
-                    read_b(j, bf);
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) {
-                        bf16x8 af[NP];
-                        read_a(i, af);
-                        mfma_split<NP>(acc[i][j], af, bf);
-                    }
-                }
-            } else {
-                // ping-pong chunks (conv_psa_kernel): tile q's 6-MFMA chain issued with tile q-1's
-                // drain adds in its gaps (the one MFMA wave per SIMD has no partner wave to cover a
-                // chain's result latency); pixel blocks outer, the A fragments re-read per tile
-                // (register budget: one B block and one A block live)
-                floatx16 prev;
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    bf16x8 bf[NP];
-                    read_b(j, bf);
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) {
-                        bf16x8 af[NP];
-                        read_a(i, af);
-                        const floatx16 cur = mfma_split0<NP>(af, bf);
-                        if (i + j > 0) {
-                            const int q = j * TM + i - 1;
-                            drain(acc[q % TM][q / TM], prev);
-#pragma unroll
-                            for (int g = 0; g < 6; ++g) {
-                                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                            }
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                        prev = cur;
-                    }
-                }
-                drain(acc[TM - 1][TN - 1], prev);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        // the tile's epilogue: + residual (one 16-element block's loads in flight at a time), stores
-        int64_t obase[TN];
-        bool nok[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int64_t n = n0 + wn + 32 * j + li;
-            nok[j] = n < N;
-            const int64_t nc = nok[j] ? n : N - 1;
-            const int b = (int)(nc / P);
-            obase[j] = (int64_t)b * M * P + (nc - (int64_t)b * P);
-        }
-        const bool full = m0 + BM <= M && n0 + BNT <= N;
-        if (res != nullptr) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    float q[16];
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int m = min(m0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
-                        q[r] = res[obase[j] + (int64_t)m * P];
-                    }
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[i][j][r] += q[r];
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-        }
-        store_tile<TM, TN>(acc, nok, obase, m0, M, P, y, full);
-    }
+    store_tile<TM, TN>(acc, nok, obase, m0, M, P, y, m0 + BM <= M && n0 + BNT <= N, inv);
 }
 
 // ------------------------------------------------------------------ 3x3 weight gradient
@@ -2999,6 +2103,14 @@ __global__ void __launch_bounds__(256) split_relayout_kernel(const float* __rest
             s = ((int64_t)(cbk * G + gi) * Cin + ci) * T + (T - 1 - tap);
         }
         float v = src[so + s];
+        if (np == 2) {
+            // 2xfp16: the fp16 pieces of w * fp16_wscale(contraction length) (common.h split2)
+            v *= ubpl::fp16_wscale((mode == 0 ? Cin : Cout) * T);
+            const _Float16 hv = (_Float16)v;
+            dst[dof + i] = __builtin_bit_cast(uint16_t, hv);
+            dst[plane + dof + i] = __builtin_bit_cast(uint16_t, (_Float16)(v - (float)hv));
+            continue;
+        }
         for (int p = 0; p < np; ++p) {
             const __bf16 hv = (__bf16)v;
             dst[(int64_t)p * plane + dof + i] = __builtin_bit_cast(uint16_t, hv);
@@ -3078,7 +2190,11 @@ Plan fwd_plan(int Cout, int64_t N, int Ktot, int np, bool psa = false) {
 void launch_split_reduce(const float* slab, int splits, int Cout, int P, int64_t N, const float* bias,
                          const float* res, float* y, hipStream_t st);
 
-template <int BM, int KS, int NP, int BNT, int WGM = 2, int KSUB = 1, bool WS = false>
+// the accumulators' scale of a split conv: 2xfp16 (NP = 2) the weight scale of its contraction
+// length x the activation scale (common.h split2), else 1
+inline float psa_osc(int np, int ktot) { return np == 2 ? ubpl::fp16_wscale(ktot) * ubpl::FP16_ACT_SCALE : 1.f; }
+
+template <int BM, int KS, int NP, int BNT, int WGM = 2, int KSUB = 1>
 int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t wplane, const float* bias,
                const float* res, float* y, int B, int Cin, int H, int W, int pad, int Cout, const Plan& pl,
                float* slab, float* stat_part, const ubpl::BnBwdEpi& bwd, hipStream_t st) {
@@ -3086,14 +2202,20 @@ int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t w
     dim3 grid((unsigned)((N + BNT - 1) / BNT), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
     const bool split = pl.splits > 1;
     const ubpl::BnBwdEpi off{nullptr, nullptr, 0, nullptr};
-    if (!split && (stat_part || bwd.part))
-        hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM, true, KSUB>), grid, dim3(NT), 0, st, xs, xplane, wp,
-                           wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl.kchunk, nullptr, stat_part, bwd);
-    else
-        hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM, false, KSUB, WS>), grid,
-                           dim3(WS ? 2 * NT : NT), 0, st, xs, xplane, wp, wplane,
-                           bias, split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr,
-                           nullptr, off);
+    const float osc = psa_osc(NP, Cin * KS * KS);
+    if constexpr (NP != 2) {   // (epilogue partials: not on the scaled 2xfp16 accumulators)
+        if (!split && (stat_part || bwd.part)) {
+            hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM, true, KSUB>), grid, dim3(NT), 0, st, xs, xplane,
+                               wp, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl.kchunk, nullptr, stat_part, bwd,
+                               osc);
+            UBPL_LAUNCH_CHECK();
+            return 0;
+        }
+    }
+    hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM, false, KSUB>), grid,
+                       dim3(NT), 0, st, xs, xplane, wp, wplane,
+                       bias, split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr,
+                       nullptr, off, osc);
     UBPL_LAUNCH_CHECK();
     if (split) {
         launch_split_reduce(slab, pl.splits, Cout, H * W, N, bias, res, y, st);
@@ -3193,7 +2315,7 @@ UBPL_API int ubpl_conv2d_forward_split(const float* x, int B, int Cin, int H, in
                                        const float* pscale, const float* pshift, const float* res, float* y, int Ho,
                                        int Wo, float* slab, int npieces, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    if (Cin % 16 != 0 || stride != 1 || (npieces != 2 && npieces != 3)) return (int)hipErrorInvalidValue;
+    if (Cin % 16 != 0 || stride != 1 || npieces != 3) return (int)hipErrorInvalidValue;
     if ((((uintptr_t)wsplit) & 15) != 0 || (plane % 8) != 0) return (int)hipErrorInvalidValue;
     const bool pro = pscale != nullptr;
     const int64_t N = (int64_t)B * Ho * Wo;
@@ -3202,14 +2324,8 @@ UBPL_API int ubpl_conv2d_forward_split(const float* x, int B, int Cin, int H, in
 #define UBPL_FD(KS_, NP_)                                                                                     \
     return fwd_dispatch<KS_, 1, NP_>(pl, pro, x, wsplit, plane, bias, pscale, pshift, res, y, B, Cin, H, W, \
                                      Cout, Ho, Wo, slab, st)
-    if (KS == 1) {
-        if (npieces == 2) UBPL_FD(1, 2);
-        UBPL_FD(1, 3);
-    }
-    if (KS == 3) {
-        if (npieces == 2) UBPL_FD(3, 2);
-        UBPL_FD(3, 3);
-    }
+    if (KS == 1) UBPL_FD(1, 3);
+    if (KS == 3) UBPL_FD(3, 3);
 #undef UBPL_FD
     return (int)hipErrorInvalidValue;
 }
@@ -3231,18 +2347,22 @@ UBPL_API int ubpl_conv_weights_split(const float* src, uint16_t* dst, int64_t pl
 // v = relu(x*pscale + pshift) when pscale != nullptr, else x.  C % 16 == 0.
 UBPL_API int ubpl_split_activation(const float* x, int B, int C, int H, int W, const float* pscale,
                                    const float* pshift, int pad, int npieces, uint16_t* dst, int64_t plane,
-                                   void* stream) {
+                                   uint16_t* dst3, int64_t plane3, void* stream) {
     if (C % 16 != 0 || npieces < 1 || npieces > 3 || pad < 0 || (plane % 8) != 0) return (int)hipErrorInvalidValue;
+    if (dst3 != nullptr && (npieces != 2 || (plane3 % 8) != 0)) return (int)hipErrorInvalidValue;
     const int Hp = H + 2 * pad, Wp = W + 2 * pad;
     dim3 grid((unsigned)((Hp * Wp + 255) / 256), (unsigned)(C / 16), (unsigned)B);
     hipStream_t st = (hipStream_t)stream;
     const bool pro = pscale != nullptr;
-#define UBPL_SA(NP_, PRO_)                                                                                      \
-    hipLaunchKernelGGL((split_act_kernel<NP_, PRO_>), grid, dim3(256), 0, st, x, C, H, W, pscale, pshift, pad, \
-                       dst, plane)
+#define UBPL_SA(NP_, PRO_, ...)                                                                                \
+    hipLaunchKernelGGL((split_act_kernel<NP_, PRO_, ##__VA_ARGS__>), grid, dim3(256), 0, st, x, C, H, W, pscale,  \
+                       pshift, pad, dst, plane, ubpl::FP16_ACT_SCALE, dst3, plane3)
     if (npieces == 1) {   // the "bf16" precision: one piece = bf16(v)
         if (pro) UBPL_SA(1, true);
         else UBPL_SA(1, false);
+    } else if (npieces == 2 && dst3 != nullptr) {   // 2xfp16 (scaled) + the 6xbf16 image
+        if (pro) UBPL_SA(2, true, true);
+        else UBPL_SA(2, false, true);
     } else if (npieces == 2) {
         if (pro) UBPL_SA(2, true);
         else UBPL_SA(2, false);
@@ -3285,33 +2405,14 @@ PsaDispatch psa_dispatch() {
 }
 }  // namespace
 
-#if UBPL_CLOCK_STAMP
-// (diagnostic build only; not in the header) the stamps of the last launches: n <= 65536
-// (memtime delta, realtime delta) pairs
-extern "C" __attribute__((visibility("default"))) int ubpl_debug_clock_stamps(unsigned long long* out, int n) {
-    if (n < 0 || n > (1 << 16)) return (int)hipErrorInvalidValue;
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk_stamp), sizeof(unsigned long long) * n, 0,
-                                       hipMemcpyDeviceToHost);
-    if (e == hipSuccess)
-        e = hipMemcpyFromSymbol(out + n, HIP_SYMBOL(g_clk_stamp), sizeof(unsigned long long) * n,
-                                sizeof(unsigned long long) * (1 << 16), hipMemcpyDeviceToHost);
-    return (int)e;
-}
-// (the same, rows 0-3: UBPL_CLOCK_STAMP=3's four phase sums)
-extern "C" __attribute__((visibility("default"))) int ubpl_debug_clock_stamps4(unsigned long long* out, int n) {
-    if (n < 0 || n > (1 << 16)) return (int)hipErrorInvalidValue;
-    for (int q = 0; q < 4; ++q) {
-        const hipError_t e = hipMemcpyFromSymbol(out + (int64_t)q * n, HIP_SYMBOL(g_clk_stamp),
-                                                 sizeof(unsigned long long) * n,
-                                                 sizeof(unsigned long long) * (1 << 16) * q, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) return (int)e;
-    }
-    return 0;
-}
-#endif
 
 UBPL_API int ubpl_set_psa_dispatch(int halo_mode, int teams) {
-    if (halo_mode < -1 || halo_mode > 5 || teams < -1 || teams > 2) return (int)hipErrorInvalidValue;
+    if (halo_mode == -2 && teams == -2) {   // back to the environment's values (read again at the next launch)
+        g_psa_halo.store(-2);
+        g_psa_teams.store(-2);
+        return 0;
+    }
+    if (halo_mode < -1 || halo_mode > 3 || teams < -1 || teams > 2) return (int)hipErrorInvalidValue;
     psa_dispatch();                       // the environment's values are read first, then replaced
     g_psa_halo.store(halo_mode);
     g_psa_teams.store(teams);
@@ -3345,6 +2446,7 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         const char* e = getenv("UBPL_PSA_BM64W");
         return !(e && atoi(e) == 0);
     }();
+    if (npieces == 2 && (stat_part || bwd.part)) return (int)hipErrorInvalidValue;   // (6xbf16 / bf16 only)
     if (KS == 4) {   // the space-to-depth stem (ubpl_stem_s2d_split): 64-row tiles on 256 pixels
         if (pl.bm != 64 || pl.splits != 1 || (npieces != 3 && npieces != 1) || N % 256 != 0)
             return (int)hipErrorInvalidValue;
@@ -3373,31 +2475,32 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
                                                                     H, W, pad, Cout, pl, slab, stat_part, bwd, st);\
         }                                                                                                          \
     } while (0)
-    // 3x3 stride-1 pad-1 on the 6xbf16 / bf16 paths, 128- or 64-row tiles, whole-row 256-pixel
+    // 3x3 stride-1 pad-1 on the split / bf16 paths, 128- or 64-row tiles, whole-row 256-pixel
     // tiles: the input halo staged once per channel group (conv_psah_kernel).  Default
-    // (measured, tools/psa_bench.py, profiles/r04_psa_diag.txt): the 6xbf16 path on the
-    // one-halo-buffer, two-workgroups-per-CU variant (212 vs 221 us at 128 ch 64x64, 750
-    // vs 786 at 256 ch, 250 vs 295 at 64 ch 128x128, 69 vs 75 at 128 ch 32x32); the bf16
-    // path at W <= 64 (54.6 vs 59.4 us at 128 ch 64x64, 184 vs 206 at 256 ch, 22.0 vs 27.0
+    // (measured, tools/psa_bench.py, profiles/r04_psa_diag.txt): the split paths (6xbf16, 2xfp16)
+    // on the one-halo-buffer, two-workgroups-per-CU variant (6xbf16: 212 vs 221 us at 128 ch
+    // 64x64, 750 vs 786 at 256 ch, 250 vs 295 at 64 ch 128x128, 69 vs 75 at 128 ch 32x32); the
+    // bf16 path at W <= 64 (54.6 vs 59.4 us at 128 ch 64x64, 184 vs 206 at 256 ch, 22.0 vs 27.0
     // at 128 ch 32x32; 104 vs 87 at 128x128: not there).
     // halo dispatch (psa_dispatch(), read once): -1 default; 0: none (conv_psa_kernel); 1:
     // every eligible launch on the double-buffered halo (two teams where the grid fills the
     // chip); test-only through ubpl_set_psa_dispatch: 2: as 1, required (a 3x3 launch the
-    // kernel cannot take is an error); 3: the one-buffer variant for every eligible 6xbf16
-    // launch, required; 4: as 3 on the 16x16x32 form (M16: the paired-piece products, a
-    // different summation order).  The tests compare the kernels in one process; modes 0-3
-    // compute in the same order, bit for bit.
+    // kernel cannot take is an error); 3: the one-buffer variant for every eligible split-piece
+    // launch, required.  The tests compare the kernels in one process; the modes compute in
+    // the same order, bit for bit.
     const int halo_mode = psa_dispatch().halo;
-    const bool one_buf = npieces == 3 && (halo_mode >= 3 || halo_mode < 0);
+    const bool split_np = npieces == 3 || npieces == 2;
+    const bool one_buf = split_np && (halo_mode >= 3 || halo_mode < 0);
     // the 96-wide planes: 192-pixel tiles on 128 rows whatever the plan's row block (its
     // cost model is conv_psa_kernel's), the one-buffer variant only
     const bool w96 = W == 96 && Cout % 128 == 0 && H % 2 == 0 &&
-                     ((npieces == 3 && one_buf) || (npieces == 1 && halo_mode > 0));   // (bf16: opt-in, slower)
-    const bool halo_ok = KS == 3 && pad == 1 && npieces != 2 && pl.splits == 1 && !stat_part && !bwd.part &&
+                     ((split_np && one_buf) || (npieces == 1 && halo_mode > 0));   // (bf16: opt-in, slower)
+    const bool halo_ok = KS == 3 && pad == 1 && pl.splits == 1 && !stat_part && !bwd.part &&
                          (((pl.bm == 128 || bm64w) && (W == 32 || W == 64 || W == 128) && H % (256 / W) == 0) ||
                           w96);
-    if ((halo_mode >= 2) && KS == 3 && npieces != 2 && !halo_ok) return (int)hipErrorInvalidValue;
+    if ((halo_mode >= 2) && KS == 3 && !halo_ok) return (int)hipErrorInvalidValue;
     const bool halo = halo_mode < 0 ? ((npieces == 1 && W <= 64) || one_buf) : halo_mode != 0;
+    const float osc = psa_osc(npieces, Cin * KS * KS);
     if (halo && halo_ok) {
         // two 4-wave teams per workgroup (512 pixels: one halo, one A ring for both,
         // two waves per SIMD) where the grid still fills the chip; UBPL_PSA_TEAMS=1 / 2
@@ -3407,14 +2510,17 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
                             H % (512 / W) == 0;
         if (teams2) {
             const dim3 grid2((unsigned)(N / 512), (unsigned)mt);
-#define UBPL_PSAH2(W_, BM_)                                                                                       \
-    do {                                                                                                          \
-        if (npieces == 3)                                                                                         \
-            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 2>), grid2, dim3(2 * NT), 0, st, xs, xplane, wsplit, \
-                               wplane, bias, res, y, B, Cin, H, Cout);                                            \
-        else                                                                                                      \
-            hipLaunchKernelGGL((conv_psah_kernel<W_, 1, BM_, 2>), grid2, dim3(2 * NT), 0, st, xs, xplane, wsplit, \
-                               wplane, bias, res, y, B, Cin, H, Cout);                                            \
+#define UBPL_PSAH2(W_, BM_)                                                                                         \
+    do {                                                                                                            \
+        if (npieces == 3)                                                                                           \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 2>), grid2, dim3(2 * NT), 0, st, xs, xplane, wsplit,   \
+                               wplane, bias, res, y, B, Cin, H, Cout, osc);                                         \
+        else if (npieces == 2)                                                                                      \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 2, BM_, 2>), grid2, dim3(2 * NT), 0, st, xs, xplane, wsplit,   \
+                               wplane, bias, res, y, B, Cin, H, Cout, osc);                                         \
+        else                                                                                                        \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 1, BM_, 2>), grid2, dim3(2 * NT), 0, st, xs, xplane, wsplit,   \
+                               wplane, bias, res, y, B, Cin, H, Cout, osc);                                         \
     } while (0)
             if (pl.bm == 128) {
                 if (W == 64) UBPL_PSAH2(64, 128);
@@ -3431,65 +2537,35 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
             const dim3 g96((unsigned)(N / 192), (unsigned)(Cout / 128));
             if (npieces == 3)
                 hipLaunchKernelGGL((conv_psah_kernel<96, 3, 128, 1, 1, 192>), g96, dim3(NT), 0, st, xs, xplane, wsplit,
-                                   wplane, bias, res, y, B, Cin, H, Cout);
+                                   wplane, bias, res, y, B, Cin, H, Cout, osc);
+            else if (npieces == 2)
+                hipLaunchKernelGGL((conv_psah_kernel<96, 2, 128, 1, 1, 192>), g96, dim3(NT), 0, st, xs, xplane, wsplit,
+                                   wplane, bias, res, y, B, Cin, H, Cout, osc);
             else
                 hipLaunchKernelGGL((conv_psah_kernel<96, 1, 128, 1, 2, 192>), g96, dim3(NT), 0, st, xs, xplane, wsplit,
-                                   wplane, bias, res, y, B, Cin, H, Cout);
+                                   wplane, bias, res, y, B, Cin, H, Cout, osc);
             UBPL_LAUNCH_CHECK();
             return 0;
         }
         const dim3 grid((unsigned)(N / 256), (unsigned)mt);
-        if (one_buf) {   // one halo buffer, two workgroups per CU
-            // the 16x16x32 form (UBPL_PSAH16=1)
-            // UBPL_PSAH16=1: the 16x16x32 form; 2: its tap-pair form on 64-row tiles
-            static const int m16_env = [] {
-                const char* e = std::getenv("UBPL_PSAH16");
-                return e != nullptr ? std::atoi(e) : 0;
-            }();
-            const bool pair = (halo_mode == 5 || (halo_mode < 0 && m16_env == 2)) && Cout % 64 == 0;
-            const bool m16 = halo_mode == 4 || (halo_mode < 0 && m16_env == 1);
-            if (pair) {
-                const dim3 grid64((unsigned)(N / 256), (unsigned)(Cout / 64));
-#define UBPL_PSAHP(W_)                                                                                          \
-    hipLaunchKernelGGL((conv_psah_kernel<W_, 3, 64, 1, 1, 256, true, true>), grid64, dim3(NT), 0, st, xs, xplane, \
-                       wsplit, wplane, bias, res, y, B, Cin, H, Cout)
-                if (W == 64) UBPL_PSAHP(64);
-                else if (W == 128) UBPL_PSAHP(128);
-                else UBPL_PSAHP(32);
-#undef UBPL_PSAHP
-                UBPL_LAUNCH_CHECK();
-                return 0;
-            }
-#define UBPL_PSAH1(W_, BM_)                                                                                   \
-    do {                                                                                                      \
-        if (m16)                                                                                              \
-            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 1, 1, 256, true>), grid, dim3(NT), 0, st, xs,    \
-                               xplane, wsplit, wplane, bias, res, y, B, Cin, H, Cout);                        \
-        else                                                                                                  \
-            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 1, 1>), grid, dim3(NT), 0, st, xs, xplane, wsplit, \
-                               wplane, bias, res, y, B, Cin, H, Cout);                                        \
-    } while (0)
-            if (pl.bm == 128) {
-                if (W == 64) UBPL_PSAH1(64, 128);
-                else if (W == 128) UBPL_PSAH1(128, 128);
-                else UBPL_PSAH1(32, 128);
-            } else {
-                if (W == 64) UBPL_PSAH1(64, 64);
-                else if (W == 128) UBPL_PSAH1(128, 64);
-                else UBPL_PSAH1(32, 64);
-            }
-#undef UBPL_PSAH1
-            UBPL_LAUNCH_CHECK();
-            return 0;
-        }
-#define UBPL_PSAH(W_, BM_)                                                                                     \
-    do {                                                                                                          \
-        if (npieces == 3)                                                                                         \
-            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane, \
-                               bias, res, y, B, Cin, H, Cout);                                                    \
-        else                                                                                                      \
-            hipLaunchKernelGGL((conv_psah_kernel<W_, 1, BM_>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane, \
-                               bias, res, y, B, Cin, H, Cout);                                                    \
+        // one halo buffer, two workgroups per CU (split pieces), or double-buffered halos
+#define UBPL_PSAH(W_, BM_)                                                                                           \
+    do {                                                                                                             \
+        if (npieces == 3 && one_buf)                                                                                 \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 1, 1>), grid, dim3(NT), 0, st, xs, xplane, wsplit,      \
+                               wplane, bias, res, y, B, Cin, H, Cout, osc);                                          \
+        else if (npieces == 2 && one_buf)                                                                            \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 2, BM_, 1, 1>), grid, dim3(NT), 0, st, xs, xplane, wsplit,      \
+                               wplane, bias, res, y, B, Cin, H, Cout, osc);                                          \
+        else if (npieces == 3)                                                                                       \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane,    \
+                               bias, res, y, B, Cin, H, Cout, osc);                                                  \
+        else if (npieces == 2)                                                                                       \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 2, BM_>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane,    \
+                               bias, res, y, B, Cin, H, Cout, osc);                                                  \
+        else                                                                                                         \
+            hipLaunchKernelGGL((conv_psah_kernel<W_, 1, BM_>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane,    \
+                               bias, res, y, B, Cin, H, Cout, osc);                                                  \
     } while (0)
         if (pl.bm == 128) {
             if (W == 64) UBPL_PSAH(64, 128);
@@ -3504,29 +2580,29 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         UBPL_LAUNCH_CHECK();
         return 0;
     }
-    if (bm64w && pl.bm == 64 && pl.splits == 1 && npieces != 2 && N % 256 == 0 && (KS == 3 || npieces == 1)) {
+    if (bm64w && pl.bm == 64 && pl.splits == 1 && N % 256 == 0 && (KS == 3 || npieces == 1)) {
         if (npieces == 3)
             return launch_psa<64, 3, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
+                                                slab, stat_part, bwd, st);
+        if (npieces == 2)
+            return launch_psa<64, 3, 2, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                                 slab, stat_part, bwd, st);
         if (KS == 3) UBPL_PSA1(64, 3, 1);
         UBPL_PSA1(64, 1, 1);
     }
-    if (bn256 && pl.bm == 128 && pl.splits == 1 && npieces != 2 && N % 256 == 0) {
+    if (bn256 && pl.bm == 128 && pl.splits == 1 && N % 256 == 0) {
         if (npieces == 1) {
             if (KS == 3) UBPL_PSA1(128, 3, 2);
             UBPL_PSA1(128, 1, 2);
         }
-        // the warp-specialized 512-thread variant (4 compute + 4 loader waves, 4-stage
-        // ring) when UBPL_PSA_WS=1 (opt-in: 350.2 vs 351.2 img/s); the
-        // epilogue-partials launches stay on 256 threads
-        static const bool ws = [] {
-            const char* e = getenv("UBPL_PSA_WS");
-            return e ? atoi(e) != 0 : PSA_WS;
-        }();
+        if (npieces == 2) {
+            if (KS == 3)
+                return launch_psa<128, 3, 2, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout,
+                                                  pl, slab, stat_part, bwd, st);
+            return launch_psa<128, 1, 2, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
+                                              slab, stat_part, bwd, st);
+        }
         if (KS == 3) {
-            if (ws && !stat_part && !bwd.part)
-                return launch_psa<128, 3, 3, 256, 2, 1, true>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W,
-                                                              pad, Cout, pl, slab, stat_part, bwd, st);
             return launch_psa<128, 3, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
                                               slab, stat_part, bwd, st);
         }
@@ -3602,7 +2678,7 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
                                              int npieces, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (!sol_supported(B, Cin, Cout, P) || (((uintptr_t)x) & 15) || (((uintptr_t)wsplit) & 15) || (wplane % 8) ||
-        (npieces != 1 && npieces != 3))
+        npieces < 1 || npieces > 3)
         return (int)hipErrorInvalidValue;
     const bool pro = pscale != nullptr;
     if (pro && Cin > SOL_PRO_K) return (int)hipErrorInvalidValue;
@@ -3611,58 +2687,39 @@ UBPL_API int ubpl_conv1x1_forward_split_load(const float* x, int B, int Cin, int
     const ubpl::BnBwdEpi bwd{bn_part ? bn_x : nullptr, bn_coef, bn_relu, bn_part};
     dim3 grid((unsigned)((N + 255) / 256), (unsigned)((Cout + bm - 1) / bm));
     const bool epi = stat_part != nullptr || bn_part != nullptr;
-    if (epi && (npieces == 1 || Cout % 64 != 0)) return (int)hipErrorInvalidValue;   // (epilogue partials: 6xbf16, whole tiles)
+    if (epi && (npieces != 3 || Cout % 64 != 0)) return (int)hipErrorInvalidValue;   // (epilogue partials: 6xbf16, whole tiles)
+    const float asc = ubpl::FP16_ACT_SCALE, osc = psa_osc(npieces, Cin);
     static const bool ns3 = sol_env("UBPL_SOL_NS", 2) == 3;
     // the activation ring 3 stages deep beside the weights' 2 (two K steps of the HBM
-    // stream in flight per workgroup); UBPL_SOL_NSB=2: one ring of 2 stages (round 4)
+    // stream in flight per workgroup; the default since round 5, measured even with the
+    // 2-stage ring, profiles/r05_v1_sol_nsb.txt); UBPL_SOL_NSB=2: one ring of 2 stages
     static const bool nsb3 = sol_env("UBPL_SOL_NSB", 3) == 3;
-    // UBPL_SOL_BN=128: 128-pixel tiles (three workgroups per CU) on the 6xbf16 path
-    static const bool bn128_env = sol_env("UBPL_SOL_BN", 256) == 128;
-    const bool bn128 = bn128_env && npieces == 3 && !epi && N % 128 == 0;
-    const dim3 grid128((unsigned)(N / 128), (unsigned)((Cout + bm - 1) / bm));
-    // the warp-specialized persistent kernel (conv1x1_ws_kernel) for 128-row tiles whose
-    // grid fills the chip; UBPL_SOL_WS=0: conv1x1_sol_kernel
-    static const bool ws_env = sol_env("UBPL_SOL_WS", 0) != 0;
-    const int64_t ntiles = ((N + 255) / 256) * ((Cout + 127) / 128);
-    if (ws_env && bm == 128 && !epi && !bn128 && ntiles >= occ_info().ncu && (!pro || Cin <= SOL_PRO_K)) {
-        const dim3 gws((unsigned)occ_info().ncu);
-#define UBPL_WS(NP_, PRO_)                                                                                        \
-    hipLaunchKernelGGL((conv1x1_ws_kernel<NP_, PRO_>), gws, dim3(2 * NT), 0, st, x, wsplit, wplane, bias, pscale,  \
-                       pshift, res, y, B, Cin, P, Cout, (int)ntiles)
-        if (npieces == 3) {
-            if (pro) UBPL_WS(3, true);
-            else UBPL_WS(3, false);
-        } else {
-            if (pro) UBPL_WS(1, true);
-            else UBPL_WS(1, false);
-        }
-#undef UBPL_WS
-        UBPL_LAUNCH_CHECK();
-        return 0;
-    }
 #define UBPL_SOL(BM_, PRO_)                                                                                       \
     do {                                                                                                          \
-        if (bn128)                                                                                                \
-            hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 3, 2, 128>), grid128, dim3(NT), 0, st, x,    \
-                               wsplit, wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);      \
-        else if (npieces == 1 && nsb3)                                                                            \
+        if (npieces == 1 && nsb3)                                                                                 \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 1, 2, 256, 3>), grid, dim3(NT), 0, st, x,    \
-                               wsplit, wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);      \
+                               wsplit, wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd, asc, osc); \
         else if (npieces == 1)                                                                                    \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 1>), grid, dim3(NT), 0, st, x, wsplit,       \
-                               wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);              \
+                               wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd, asc, osc);    \
+        else if (npieces == 2 && nsb3)                                                                            \
+            hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 2, 2, 256, 3>), grid, dim3(NT), 0, st, x,    \
+                               wsplit, wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd, asc, osc); \
+        else if (npieces == 2)                                                                                    \
+            hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 2>), grid, dim3(NT), 0, st, x, wsplit,       \
+                               wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd, asc, osc);    \
         else if (BM_ == 64 && ns3 && !epi)                                                                        \
             hipLaunchKernelGGL((conv1x1_sol_kernel<64, PRO_, false, 3, 3>), grid, dim3(NT), 0, st, x, wsplit,     \
-                               wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);              \
+                               wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd, asc, osc);    \
         else if (epi)                                                                                             \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, true>), grid, dim3(NT), 0, st, x, wsplit, wplane,   \
-                               bias, pscale, pshift, res, y, B, Cin, P, Cout, stat_part, bwd);                    \
+                               bias, pscale, pshift, res, y, B, Cin, P, Cout, stat_part, bwd, asc, osc);          \
         else if (nsb3)                                                                                            \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_, false, 3, 2, 256, 3>), grid, dim3(NT), 0, st, x,    \
-                               wsplit, wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);      \
+                               wsplit, wplane, bias, pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd, asc, osc); \
         else                                                                                                      \
             hipLaunchKernelGGL((conv1x1_sol_kernel<BM_, PRO_>), grid, dim3(NT), 0, st, x, wsplit, wplane, bias,   \
-                               pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd);                            \
+                               pscale, pshift, res, y, B, Cin, P, Cout, nullptr, bwd, asc, osc);                  \
     } while (0)
     if (bm == 128) {
         if (pro) UBPL_SOL(128, true);

@@ -68,7 +68,7 @@ SIGNATURES = {
     "ubpl_conv2d_forward_split_workspace": (L, [I, I, I, I, I, I, I]),
     "ubpl_conv2d_forward_split": (I, [P, I, I, I, I, P, L, P, I, I, I, P, P, P, P, I, I, P, I, P]),
     "ubpl_conv_weights_split": (I, [P, P, L, P, I, I, I, P]),
-    "ubpl_split_activation": (I, [P, I, I, I, I, P, P, I, I, P, L, P]),
+    "ubpl_split_activation": (I, [P, I, I, I, I, P, P, I, I, P, L, P, L, P]),
     "ubpl_conv2d_forward_psa_workspace": (L, [I, I, I, I, I, I, I]),
     "ubpl_set_psa_dispatch": (I, [I, I]),
     "ubpl_conv2d_forward_psa": (I, [P, L, I, I, I, I, I, P, L, P, I, I, P, P, P, I, P, P, P, I, P, P]),

@@ -19,12 +19,19 @@ BatchNorm running statistics are per-rank (train-mode teachers keep their
 own); `broadcast_buffers` syncs them from rank 0 before validation or a
 checkpoint.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
+# UBPL_DIST_WORLD1=1: the distributed step (its two collectives, the segmented capture of
+# train._StepGraph) also on a one-rank process group — how the RCCL path is exercised on a
+# one-GPU box (tests/test_gpu_dist.py; RCCL refuses two ranks on one device)
+_WORLD1 = os.environ.get("UBPL_DIST_WORLD1") == "1"
+
 
 def is_dist():
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or _WORLD1)
 
 
 def rank():

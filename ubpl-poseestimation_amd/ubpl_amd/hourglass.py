@@ -255,8 +255,9 @@ class StackedHourglass(nn.Module):
                  PSA path, error at the f32 path's level), the 1x1 convs whose
                  planes fill the chip on the same arithmetic with the activations
                  split while they are staged, the rest f32;
-        '3xbf16' every conv with 16-channel contraction groups on the 2-piece
-                 register-staged split kernel (faster, ~2^-16 operands: not parity-grade);
+        '2xfp16' the forward convs as '6xbf16' places them, on 2 fp16 pieces of the
+                 power-of-two-scaled operands (3 MFMA products instead of 6, operands
+                 to 2^-22); the backward (data and weight gradients) on 6xbf16;
         'bf16'   every conv with 16-channel contraction groups (3x3 and 1x1, forward
                  and data gradient) with ONE piece per operand = bf16 operands, f32
                  accumulation (BASELINE config 5's throughput path): 1x1 convs whose
@@ -266,7 +267,8 @@ class StackedHourglass(nn.Module):
                  weight gradients exact f32.
         The stem (7x7, stride 2, 3 input channels) runs in f32 except on the
         6xbf16 space-to-depth path."""
-        self.conv_pieces = Kn.conv_precision_pieces(name)
+        self.conv_pieces = Kn.conv_precision_pieces(name)          # the forward's
+        self.bwd_pieces = Kn.backward_pieces(self.conv_pieces)      # the gradients'
         self._build_weight_tables()
 
     def _build_weight_tables(self):
@@ -276,16 +278,16 @@ class StackedHourglass(nn.Module):
         re-layout, _wlay[("rest", mode)] = those of them not on the split path."""
         tab, offs, device = self._table, self._offs, self._device
         stem = "pre.0.conv.weight"
-        pieces = self.conv_pieces
         self._wsp = {}
         for mode in (0, 1):
+            pieces = self.conv_pieces if mode == 0 else self.bwd_pieces
             rows, idx, o = [], {}, 0
             for name, shape, kind, live in tab:
                 if kind != "cw" or not live or name == stem or not pieces or shape[1 if mode == 0 else 0] % 16:
                     continue
-                # 6xbf16: 3x3 (PSA path) and 1x1 (split on load; outputs of 16 channels and up,
-                # the heatmap projection included)
-                if pieces == 3 and not (shape[2] == 3 or (shape[2] == 1 and shape[0 if mode == 0 else 1] % 16 == 0)):
+                # 6xbf16 / 2xfp16: 3x3 (PSA path) and 1x1 (split on load; outputs of 16 channels
+                # and up, the heatmap projection included)
+                if pieces in (2, 3) and not (shape[2] == 3 or (shape[2] == 1 and shape[0 if mode == 0 else 1] % 16 == 0)):
                     continue
                 s, n, _ = offs[name]
                 T = shape[2] * shape[3]
@@ -293,7 +295,8 @@ class StackedHourglass(nn.Module):
                 idx[name] = (o, (shape[0], T, shape[1]) if mode == 0 else (shape[1], T, shape[0]))
                 o += (n + 7) // 8 * 8
             buf = torch.empty(max(pieces, 1) * max(o, 8), dtype=torch.int16, device=device)
-            self._wsp[mode] = [torch.tensor(rows, dtype=torch.int64).reshape(-1, 5).to(device), max(o, 8), idx, buf]
+            self._wsp[mode] = [torch.tensor(rows, dtype=torch.int64).reshape(-1, 5).to(device), max(o, 8), idx, buf,
+                               pieces]
         self._wlay = {}
         for mode in (0, 1):
             need = (lambda ks, nm: ks > 1) if mode == 0 else (lambda ks, nm: nm != stem)
@@ -314,8 +317,8 @@ class StackedHourglass(nn.Module):
 
     def relayout_weights(self, mode):
         if self.conv_pieces:
-            tbl, plane, _, buf = self._wsp[mode]
-            Kn.conv_weights_split(self.flat_params, buf, plane, tbl, mode, self.conv_pieces)
+            tbl, plane, _, buf, pieces = self._wsp[mode]
+            Kn.conv_weights_split(self.flat_params, buf, plane, tbl, mode, pieces)
             tbl, buf, _, m = self._wlay[("rest", mode)]
             if tbl.shape[0]:
                 Kn.conv_weights_relayout(self.flat_params, buf, tbl, m)
@@ -331,11 +334,11 @@ class StackedHourglass(nn.Module):
 
     def SW(self, mode, name):
         """Split-bf16 weights of a conv (None when it is not on the split path)."""
-        _, plane, idx, buf = self._wsp[mode]
+        _, plane, idx, buf, pieces = self._wsp[mode]
         if not self.conv_pieces or name not in idx:
             return None
         o, shp = idx[name]
-        return Kn.SplitWeights(buf, plane, o, shp, self.conv_pieces)
+        return Kn.SplitWeights(buf, plane, o, shp, pieces)
 
     def alt_grad_buffer(self):
         """Second gradient buffer for a backward pass that runs concurrently with
@@ -608,18 +611,25 @@ class _Exec:
         mkpart = lambda: (Kn.bn_partial_buffer(Cout, B * x.shape[2] * x.shape[3], x.device)
                           if stats and _FWD_EPI else None)
         ws = self.m.SW(0, name + ".weight") if stride == 1 else None
-        if ws is not None and ws.npieces in (1, 3) and ws.shape[1] == 1:
+        if ws is not None and ws.npieces in (1, 2, 3) and ws.shape[1] == 1:
             if Kn.conv1x1_split_load_ok(x, ws):
                 part = mkpart() if ws.npieces == 3 else None
                 return Kn.conv1x1_forward_split_load(x, ws, b, ps, ph, res=res, out=out, stat_part=part), part
-            if ws.npieces == 3:
+            if ws.npieces in (2, 3):
                 ws = None                                # small plane: the f32 1x1 kernel (bf16: the PSA kernel)
         if ws is not None:
-            if ws.npieces in (1, 3):
-                part = mkpart()
-                xs = Kn.split_activation(x, ws.npieces, (ws.shape[1] == 9) * 1, ps, ph)
-                if self.do_save and ws.shape[1] == 9:
-                    self.saved_split[name] = xs          # the 3x3 weight gradient's B operand
+            if ws.npieces in (1, 2, 3):
+                part = mkpart() if ws.npieces != 2 else None
+                keep = self.do_save and ws.shape[1] == 9
+                if ws.npieces == 2 and keep:
+                    # 2xfp16: the conv's fp16 image and, from the same read, the 6xbf16 one
+                    # its weight gradient takes
+                    xs, xs3 = Kn.split_activation(x, 2, 1, ps, ph, with3=True)
+                    self.saved_split[name] = xs3
+                else:
+                    xs = Kn.split_activation(x, ws.npieces, (ws.shape[1] == 9) * 1, ps, ph)
+                    if keep:
+                        self.saved_split[name] = xs      # the 3x3 weight gradient's B operand
                 return Kn.conv2d_forward_psa(xs, ws, b, res=res, out=out, stat_part=part), part
             return Kn.conv2d_forward_split(x, ws, b, ps, ph, res=res, out=out), None
         if w.shape[2] == 1 and stride == 1 and Kn.conv1x1_kmajor_ok(x, w.shape[0]):
@@ -631,10 +641,11 @@ class _Exec:
 
     # ---- layers
     def stem(self, imgs):
-        if self.m.conv_pieces in (1, 3) and _STEM_S2D and Kn.stem_s2d_ok(imgs):
+        if self.m.conv_pieces in (1, 2, 3) and _STEM_S2D and Kn.stem_s2d_ok(imgs):
             # 7x7/s2 as a 4x4 stride-1 conv over the space-to-depth image, on the split path
-            # (6xbf16), or on bf16 operands (the "bf16" precision)
-            np_ = self.m.conv_pieces
+            # (6xbf16, also under 2xfp16: the image is its weight gradient's operand), or on
+            # bf16 operands (the "bf16" precision)
+            np_ = self.m.bwd_pieces
             ws = Kn.stem_weight_s2d_split(self.m.P("pre.0.conv.weight"), np_)
             xs = Kn.stem_s2d_split(imgs, 2, np_)
             y0 = Kn.conv2d_forward_psa(xs, ws, self.m.P("pre.0.conv.bias"))
@@ -717,13 +728,13 @@ class _Exec:
         sc, sh, mu, istd = self.bnc(name)
         return Kn.bn_backward_split(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.bpart,
                                     self._coef(), self.G(name + ".weight"), self.G(name + ".bias"),
-                                    self.m.conv_pieces, 1, part=part)
+                                    self.m.bwd_pieces, 1, part=part)
 
     def wgrad(self, name, dy, x, KS, stride=1, pro=None):
         ps, ph = (None, None) if pro is None else pro
-        if KS == 1 and self.m.conv_pieces in (1, 3) and _WGRAD1_SPLIT and Kn.wgrad1x1_split_load_ok(dy, x):
+        if KS == 1 and self.m.bwd_pieces in (1, 3) and _WGRAD1_SPLIT and Kn.wgrad1x1_split_load_ok(dy, x):
             Kn.conv2d_wgrad1x1_split_load(dy, x, self.G(name + ".weight"), self.G(name + ".bias"), ps, ph,
-                                          accumulate=True, npieces=self.m.conv_pieces)
+                                          accumulate=True, npieces=self.m.bwd_pieces)
             return
         Kn.conv2d_wgrad(dy, x, KS, stride, self.G(name + ".weight"), self.G(name + ".bias"), ps, ph,
                         accumulate=True)
@@ -857,7 +868,7 @@ class _Exec:
         imgs, y0 = self.saved.get("pre.0")
         xs = self.saved_split.get("pre.0.conv")
         w0 = m.P("pre.0.conv.weight")
-        if xs is not None and m.conv_pieces in (1, 3) and d.shape[1] % 64 == 0 and d.shape[3] % 16 == 0:
+        if xs is not None and m.bwd_pieces in (1, 3) and d.shape[1] % 64 == 0 and d.shape[3] % 16 == 0:
             # dy of the stem only as the split operand of its weight gradient (the input
             # image takes no gradient): the space-to-depth 4x4 weight gradient, mapped to 7x7
             ys = self.bn_bwd_split("pre.0.bn", d, y0, relu=1)

@@ -384,13 +384,23 @@ def conv_weights_relayout(src, dst, table, mode):
     call("ubpl_conv_weights_relayout", _p(src), _p(dst), _p(table), int(table.shape[0]), int(mode))
 
 
-# Conv arithmetic: "f32" = exact-f32 MFMA (v_mfma_f32_32x32x2_f32); "3xbf16" /
-# "6xbf16" = split-bf16 MFMA with 2 / 3 bf16 pieces per f32 operand (3 / 6
-# piece products, f32 accumulation); "bf16" = one piece, i.e. both operands
-# rounded to bf16 (RNE) with f32 accumulation — the throughput precision of
-# BASELINE config 5 (8 stacks, 384x384), not parity-grade.  Value = pieces (0 for f32).
-CONV_PRECISIONS = {"f32": 0, "bf16": 1, "3xbf16": 2, "6xbf16": 3}
+# Conv arithmetic: "f32" = exact-f32 MFMA (v_mfma_f32_32x32x2_f32); "6xbf16" =
+# split-bf16 MFMA with 3 bf16 pieces per f32 operand (6 piece products, f32
+# accumulation: exact operands); "2xfp16" = the forward convs (students' and
+# teachers') with 2 fp16 pieces per operand of the power-of-two-scaled value (3
+# piece products on the fp16 MFMA, operands to 2^-22: conv_split.hip / common.h
+# split2), the backward (data and weight gradients, whose operands have no
+# known range) on 6xbf16; "bf16" = one piece, i.e. both operands rounded to bf16
+# (RNE) with f32 accumulation — the throughput precision of BASELINE config 5
+# (8 stacks, 384x384), not parity-grade.  Value = the forward's pieces (0 for f32).
+CONV_PRECISIONS = {"f32": 0, "bf16": 1, "2xfp16": 2, "6xbf16": 3}
 DEFAULT_CONV_PRECISION = "6xbf16"
+
+
+def backward_pieces(pieces):
+    """Pieces of the data / weight gradients' split operands for a precision's
+    forward pieces (2xfp16: the backward runs on 6xbf16)."""
+    return 3 if pieces == 2 else pieces
 
 
 def conv_precision_name(name=None):
@@ -457,8 +467,9 @@ def conv2d_forward_split(x, ws, bias, pscale=None, pshift=None, res=None, out=No
 
 
 class SplitAct:
-    """Pre-split activations (conv_split.hip PSA layout): `npieces` bf16 planes of
-    [B][C/16][H+2pad][W+2pad][16] in an int16 buffer, planes `plane` elements apart."""
+    """Pre-split activations (conv_split.hip PSA layout): `npieces` 16-bit planes of
+    [B][C/16][H+2pad][W+2pad][16] in an int16 buffer, planes `plane` elements apart
+    (3: bf16 pieces; 2: fp16 pieces of v * 32, the 2xfp16 path; 1: bf16(v))."""
 
     __slots__ = ("buf", "plane", "B", "C", "H", "W", "pad", "npieces")
 
@@ -467,15 +478,23 @@ class SplitAct:
         self.pad, self.npieces = pad, npieces
 
 
-def split_activation(x, npieces, pad, pscale=None, pshift=None, out=None):
-    """x [B,C,H,W] f32 -> SplitAct of relu(x*pscale + pshift) (or x), zero border `pad`."""
+def split_activation(x, npieces, pad, pscale=None, pshift=None, out=None, with3=False):
+    """x [B,C,H,W] f32 -> SplitAct of relu(x*pscale + pshift) (or x), zero border `pad`.
+    with3 (npieces 2): (the 2xfp16 image, the 3-piece 6xbf16 image) from one read — the
+    2xfp16 forward's conv input and the 6xbf16 weight gradient's operand."""
     B, C, H, W = x.shape
     plane = B * C * (H + 2 * pad) * (W + 2 * pad)
     if out is None:
         out = torch.empty(npieces * plane, device=x.device, dtype=torch.int16)
+    out3 = None
+    if with3:
+        if npieces != 2:
+            raise ValueError("with3: the 2xfp16 split only")
+        out3 = torch.empty(3 * plane, device=x.device, dtype=torch.int16)
     call("ubpl_split_activation", _p(x), B, C, H, W, _p(pscale), _p(pshift), int(pad), int(npieces), _p(out),
-         int(plane))
-    return SplitAct(out, plane, B, C, H, W, pad, npieces)
+         int(plane), _p(out3), int(plane))
+    xs = SplitAct(out, plane, B, C, H, W, pad, npieces)
+    return (xs, SplitAct(out3, plane, B, C, H, W, pad, 3)) if with3 else xs
 
 
 def conv2d_forward_psa(xs, ws, bias, res=None, out=None, stat_part=None, bwd=None):
@@ -526,9 +545,9 @@ _NO_SOL = os.environ.get("UBPL_NO_SOL") == "1"      # diagnostic: every 1x1 on t
 
 
 def conv1x1_split_load_ok(x, ws):
-    """The split-on-load 1x1 kernel (6xbf16 or bf16) takes this shape and fills the chip."""
+    """The split-on-load 1x1 kernel (6xbf16, 2xfp16 or bf16) takes this shape and fills the chip."""
     B, Cin, H, W = x.shape
-    return (not _NO_SOL and ws is not None and ws.npieces in (1, 3) and ws.shape[1] == 1 and ws.shape[2] == Cin
+    return (not _NO_SOL and ws is not None and ws.npieces in (1, 2, 3) and ws.shape[1] == 1 and ws.shape[2] == Cin
             and x.data_ptr() % 16 == 0
             and bool(_lib.lib().ubpl_conv1x1_split_load_preferred(B, Cin, ws.shape[0], H * W)))
 
@@ -544,14 +563,14 @@ def _bnb(bwd):
 
 def conv1x1_forward_split_load(x, ws, bias, pscale=None, pshift=None, res=None, out=None, stat_part=None,
                                bwd=None):
-    """1x1 stride-1 conv on the split path (ws.npieces 3: 6xbf16; 1: bf16 operands)
+    """1x1 stride-1 conv on the split path (ws.npieces 3: 6xbf16; 2: 2xfp16; 1: bf16 operands)
     with x (NCHW f32) split while it is staged: y = conv(relu(x*pscale + pshift) or x, ws) + bias (+ res; res may
     alias out); ws = SplitWeights (rows, 1, Cin) — a forward (mode 0) or a data
     gradient (mode 1, x = dy) table; stat_part: BatchNorm partials of y."""
     B, Cin, H, W = x.shape
     Cout, T, wc = ws.shape
-    if T != 1 or wc != Cin or ws.npieces not in (1, 3) or (ws.npieces == 1 and (stat_part is not None or
-                                                                            bwd is not None)):
+    if T != 1 or wc != Cin or ws.npieces not in (1, 2, 3) or (ws.npieces != 3 and (stat_part is not None or
+                                                                               bwd is not None)):
         raise AssertionError("split-load 1x1: weights {} / pieces {} for {} input channels".format(
             ws.shape, ws.npieces, Cin))
     y = torch.empty((B, Cout, H, W), device=x.device, dtype=F32) if out is None else out
@@ -705,7 +724,7 @@ def augment_chain(imgs, geo, cs, noise, img_mean, chan_mean, Hm, Wm, out):
         raise ValueError("augment_chain: a crop %.3fx the output size needs skimage's anti-aliasing blur "
                          "(sigma %.3f px), which the device resize does not run; crops up to 1.3x are exact"
                          % (s, (s - 1) / 2))
-    inter =torch.empty((V, 3, Hm, Wm), device=out.device, dtype=F32)
+    inter = torch.empty((V, 3, Hm, Wm), device=out.device, dtype=F32)
     call("ubpl_augment_chain", _p(imgs), imgs.shape[1], imgs.shape[2], _p(geo), _p(cs), _p(noise), _p(img_mean),
          _p(chan_mean), V, int(Hm), int(Wm), _p(inter), Ho, Wo, _p(out))
     return out

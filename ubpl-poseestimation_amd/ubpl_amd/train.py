@@ -301,21 +301,40 @@ class _ModelStreams:
             s.wait_stream(self.main)
         if _STREAM_CHECK and self._check is None:
             self._check = _PhaseCheck().__enter__()
+            _OPEN_CHECKS.append(self)
+
+    def end_check(self):
+        """Leave the phase's _PhaseCheck mode (if one is on); returns what it saw."""
+        if self._check is None:
+            return ()
+        chk, self._check = self._check, None
+        chk.__exit__(None, None, None)
+        if self in _OPEN_CHECKS:
+            _OPEN_CHECKS.remove(self)
+        return chk.seen
 
     def join(self, tensors=()):
-        if self._check is not None:
-            chk, self._check = self._check, None
-            chk.__exit__(None, None, None)
-            if chk.seen:
-                raise RuntimeError("ubpl_amd: PyTorch arithmetic enqueued while the network streams run "
-                                   "(UBPL_STREAM_CHECK): %s" % sorted(set(chk.seen)))
+        seen = self.end_check()
         for s in self.side:
             self.main.wait_stream(s)
+        if seen:                          # (main has joined every network stream first)
+            raise RuntimeError("ubpl_amd: PyTorch arithmetic enqueued while the network streams run "
+                               "(UBPL_STREAM_CHECK): %s" % sorted(set(seen)))
         if torch.cuda.is_current_stream_capturing():
             return                        # the graph's own dependencies order them
         for t in tensors:                 # produced on a side stream, used on main
             if t is not None and t.is_cuda:
                 t.record_stream(self.main)
+
+
+# phases whose _PhaseCheck mode is on (UBPL_STREAM_CHECK): a step that raised between a
+# fork and its join leaves its mode on the dispatch stack; the step drivers close them
+_OPEN_CHECKS = []
+
+
+def _close_phase_checks():
+    while _OPEN_CHECKS:
+        _OPEN_CHECKS[-1].end_check()
 
 
 # The students' gradient all-reduce runs after the network streams have joined,
@@ -363,6 +382,8 @@ def _drive(gen):
             req = gen.send(None)
     except StopIteration as e:
         return e.value
+    finally:
+        _close_phase_checks()
 
 
 # AdamW + the EMA teacher update in one pass per model (FlatAdamW.step_and_ema);
@@ -608,17 +629,20 @@ class _StepGraph:
             return
         pool = torch.cuda.graph_pool_handle()
         graphs, reqs, done = [], [], False
-        while not done:
-            g = torch.cuda.CUDAGraph()
-            # thread_local: the process group's own threads may query HIP while a segment captures
-            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
-                try:
-                    req = gen.send(None)
-                except StopIteration as e:
-                    self.out, done = e.value, True
-            graphs.append(g)
-            if not done:
-                reqs.append(req)
+        try:
+            while not done:
+                g = torch.cuda.CUDAGraph()
+                # thread_local: the process group's own threads may query HIP while a segment captures
+                with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+                    try:
+                        req = gen.send(None)
+                    except StopIteration as e:
+                        self.out, done = e.value, True
+                graphs.append(g)
+                if not done:
+                    reqs.append(req)
+        finally:
+            _close_phase_checks()
         self.graphs, self.reqs = graphs, reqs
 
     def run(self, batch, dev):
@@ -860,14 +884,26 @@ def _mt_ubpl_records(host, bat, meta_h, M, pec_c, mtc_c, epc_c, fdc_c, args, ver
         fdc_c.update(host[3 * M], int(sum(host[nrec + 3 * M:nrec + 3 * M + nf])))
     else:
         fdc_c.update(0., B)
-    if verbose and use_ep:
+    if use_ep:
         n_ps = int(sum(host[nrec + 3 * mi + 1] for mi in range(M)))
         n_sel = int(sum(host[nrec + 3 * mi + 2] for mi in range(M)))
-        sc = host[nrec + ncn:]
-        print("batch.{} (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
-            format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
-            format(n_sel / n_ps if n_ps else float("nan"), ".2f"), format(n_sel, "5d"), format(n_ps, "5d"),
-            ", ".join(format(v, ".3f") for v in sc)))
+        # the reference's batch line divides by the pseudo-label count whether or not it
+        # prints anywhere (projects/MT_UBPL.py:292-293, integer counts): a step with none
+        # raises ZeroDivisionError there, and here when its records are consumed
+        rate = _pseudo_rate(n_sel, n_ps)
+        if verbose:
+            sc = host[nrec + ncn:]
+            print("batch.{} (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
+                format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
+                format(rate, ".2f"), format(n_sel, "5d"), format(n_ps, "5d"),
+                ", ".join(format(v, ".3f") for v in sc)))
+
+
+def _pseudo_rate(n_sel, n_ps):
+    """n_sel / n_ps as the reference's batch line computes it: Python ints, so a step
+    without pseudo labels raises ZeroDivisionError (projects/MT_UBPL.py:292-293,
+    DualPose_UBPL.py:212-213,238-239)."""
+    return int(n_sel) / int(n_ps)
 
 
 def _fdl_rows(sw, args):
@@ -1008,20 +1044,22 @@ def _dualpose_records(host, bat, ncn, K, use_ep, nfd, M, S, pec_c, mtc_c, epc_c,
         fdc_c.update(host[3 * M], int(host[cbase + 6 * M]))
     else:
         fdc_c.update(0., S)                                   # :249 outs.shape[2] = nStack
+    off = cbase + ncn
+    c_ps = int(sum(host[cbase + 6 * mi + 3] for mi in range(M)))
+    c_sel = int(sum(host[cbase + 6 * mi + 4] for mi in range(M)))
+    e_ps = int(sum(host[cbase + 6 * mi + 2] for mi in range(M)))
+    e_sel = int(sum(host[cbase + 6 * mi + 5] for mi in range(M)))
+    c_rate = _pseudo_rate(c_sel, c_ps)                        # (the reference's lines raise on a zero count)
+    e_rate = _pseudo_rate(e_sel, e_ps) if use_ep else None
     if verbose:
-        off = cbase + ncn
-        c_ps = int(sum(host[cbase + 6 * mi + 3] for mi in range(M)))
-        c_sel = int(sum(host[cbase + 6 * mi + 4] for mi in range(M)))
-        e_ps = int(sum(host[cbase + 6 * mi + 2] for mi in range(M)))
-        e_sel = int(sum(host[cbase + 6 * mi + 5] for mi in range(M)))
         print("batch.{} consist-pseudo (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
             format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
-            format(c_sel / c_ps if c_ps else float("nan"), ".2f"), format(c_sel, "5d"), format(c_ps, "5d"),
+            format(c_rate, ".2f"), format(c_sel, "5d"), format(c_ps, "5d"),
             ", ".join(format(v, ".3f") for v in host[off:off + K])))
         if use_ep:
             print("batch.{} ensemble-pseudo (scoreThr:{}): {} ({}/{}), pseudo-score: [{}]".format(
                 format(bat + 1, "5d"), format(args.pseudoScoreThr, ".2f"),
-                format(e_sel / e_ps if e_ps else float("nan"), ".2f"), format(e_sel, "5d"), format(e_ps, "5d"),
+                format(e_rate, ".2f"), format(e_sel, "5d"), format(e_ps, "5d"),
                 ", ".join(format(v, ".3f") for v in host[off + K:off + 2 * K])))
 
 
