@@ -156,9 +156,12 @@ int ubpl_bn_backward(const float* dz, const float* x, int B, int C, int HW, cons
                      const float* part, float* coef, float* dgamma, float* dbeta, const float* add1,
                      const float* add2, float* dx, void* stream);
 /* The same backward with dx delivered only as PSA planes (ubpl_split_activation
- * layout, border `pad`, npieces 2 or 3) — the operand of a split-path 3x3 data /
- * weight gradient; no addends; C % 16 == 0. */
-/*@ dz:f32[(int64_t)B*C*H*W] x:f32[(int64_t)B*C*H*W] gamma:f32[C] mean:f32[C] invstd:f32[C] scale:f32[C] shift:f32[C] scratch:f64[ubpl_bn_part_doubles(B,C)] part:f32[ubpl_bn_partial_floats(C,(int64_t)B*H*W)] coef:f32[3*C] dgamma:f32[C] dbeta:f32[C] dst:u16[(npieces-1)*plane+(int64_t)B*C*(H+2*pad)*(W+2*pad)] */
+ * layout, border `pad`, npieces 1, 2 or 3) — the operand of a split-path 3x3 data /
+ * weight gradient; no addends; C % 16 == 0.  npieces 2 (2xfp16): the statistics
+ * pass also bounds |dx| and picks the power-of-two scale of the fp16 pieces,
+ * written to coef[3C] (coef: 3C + 1 floats) for the consumers (act_scale of
+ * ubpl_conv2d_forward_psa / dscale of ubpl_wgrad3_psa); not with `part`. */
+/*@ dz:f32[(int64_t)B*C*H*W] x:f32[(int64_t)B*C*H*W] gamma:f32[C] mean:f32[C] invstd:f32[C] scale:f32[C] shift:f32[C] scratch:f64[ubpl_bn_part_doubles(B,C)] part:f32[ubpl_bn_partial_floats(C,(int64_t)B*H*W)] coef:f32[3*C+1] dgamma:f32[C] dbeta:f32[C] dst:u16[(npieces-1)*plane+(int64_t)B*C*(H+2*pad)*(W+2*pad)] */
 int ubpl_bn_backward_split(const float* dz, const float* x, int B, int C, int H, int W, const float* gamma,
                            const float* mean, const float* invstd, const float* scale, const float* shift, int relu,
                            double* scratch, const float* part, float* coef, float* dgamma, float* dbeta, int pad,
@@ -257,12 +260,14 @@ int64_t ubpl_conv2d_forward_psa_workspace(int B, int Cin, int Cout, int KS, int 
 int ubpl_set_psa_dispatch(int halo_mode, int teams);
 /* 3x3 weight gradient (+ bias gradient, db nullable) on the split path from PSA
  * operands with a 1-pixel border: dys = split(dy), xs = split(conv input),
- * npieces = 3; Cin % 64 == 0, Cout % 64 == 0, W % 16 == 0. */
+ * npieces 3 (6xbf16), 1 (bf16) or 2 (2xfp16: dys the pieces of dy * *dscale —
+ * ubpl_bn_backward_split's coef[3C] — and xs of x * 32, the forward's image;
+ * dscale required exactly then); Cin % 64 == 0, Cout % 64 == 0, W % 16 == 0. */
 int64_t ubpl_wgrad3_psa_workspace(int B, int Cin, int Cout, int H, int W);
-/*@ dys:u16[(npieces-1)*dplane+(int64_t)B*Cout*(H+2)*(W+2)] xs:u16[(npieces-1)*xplane+(int64_t)B*Cin*(H+2)*(W+2)] slab:f32[ubpl_wgrad3_psa_workspace(B,Cin,Cout,H,W)] dw:f32[(int64_t)Cout*Cin*9] db:f32[Cout] */
+/*@ dys:u16[(npieces-1)*dplane+(int64_t)B*Cout*(H+2)*(W+2)] xs:u16[(npieces-1)*xplane+(int64_t)B*Cin*(H+2)*(W+2)] slab:f32[ubpl_wgrad3_psa_workspace(B,Cin,Cout,H,W)] dw:f32[(int64_t)Cout*Cin*9] db:f32[Cout] dscale:f32[1] */
 int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int Cin,
                     int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,
-                    void* stream);
+                    const float* dscale, void* stream);
 /* The 7x7 stride-2 stem's weight gradient (+ bias gradient, db nullable) on the
  * split path, as the weight gradient of its space-to-depth form (replaces the
  * exact-f32 ubpl_conv2d_wgrad for models/pose/hourglass.py pre.0 / layers.py:31-50):
@@ -284,15 +289,19 @@ int64_t ubpl_wgrad1x1_split_load_workspace(int B, int Cin, int Cout, int P);
 int ubpl_wgrad1x1_split_load(const float* dy, const float* x, int B, int Cin, int Cout, int P, const float* pscale,
                              const float* pshift, float* slab, float* dw, float* db, int accumulate, int npieces,
                              void* stream);
-/*@ xs:u16[(npieces-1)*xplane+(int64_t)B*Cin*(H+2*pad)*(W+2*pad)] wsplit:u16[(npieces-1)*wplane+(int64_t)Cout*Cin*KS*KS] bias:f32[Cout] res:f32[(int64_t)B*Cout*H*W] y:f32[(int64_t)B*Cout*H*W] slab:f32[ubpl_conv2d_forward_psa_workspace(B,Cin,Cout,KS,H,W,npieces)] stat_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*H*W)] bn_x:f32[(int64_t)B*Cout*H*W] bn_coef:f32[3*Cout] bn_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*H*W)] */
+/*@ xs:u16[(npieces-1)*xplane+(int64_t)B*Cin*(H+2*pad)*(W+2*pad)] wsplit:u16[(npieces-1)*wplane+(int64_t)Cout*Cin*KS*KS] bias:f32[Cout] res:f32[(int64_t)B*Cout*H*W] y:f32[(int64_t)B*Cout*H*W] slab:f32[ubpl_conv2d_forward_psa_workspace(B,Cin,Cout,KS,H,W,npieces)] stat_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*H*W)] bn_x:f32[(int64_t)B*Cout*H*W] bn_coef:f32[3*Cout] bn_part:f32[ubpl_bn_partial_floats(Cout,(int64_t)B*H*W)] act_scale:f32[1] */
 int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, int Cin, int H, int W, int pad,
                             const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
                             const float* res, float* y, float* slab, int npieces, float* stat_part,
-                            const float* bn_x, const float* bn_coef, int bn_relu, float* bn_part, void* stream);
+                            const float* bn_x, const float* bn_coef, int bn_relu, float* bn_part,
+                            const float* act_scale, void* stream);
 /* bn_part (nullable; with bn_x [B,Cout,P], bn_coef = scale|shift|mean, Cout
  * floats each, bn_relu): when y is the data gradient dz of a BatchNorm(+ReLU)
  * with input bn_x, its backward statistics partials (ubpl_bn_backward layout),
- * from the epilogue — then ubpl_bn_backward(..., part_ready = 1) needs no pass. */
+ * from the epilogue — then ubpl_bn_backward(..., part_ready = 1) needs no pass.
+ * act_scale (nullable, npieces 2 only): the device-side scale of xs's pieces (a
+ * data gradient's, ubpl_bn_backward_split coef[3C]); null: xs from
+ * ubpl_split_activation (scale 32). */
 /* The 7x7 stride-2 stem (Cin <= 4) on the split path by space-to-depth: the
  * phase images of x as a 16-channel PSA image with a `pad` (>= 2) border, and
  * the equivalent 4x4 stride-1 weights (Cin' = 16, KS' = 4) split into npieces

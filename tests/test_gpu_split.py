@@ -372,6 +372,95 @@ def test_bn_backward_split_matches_f32_then_split():
             assert torch.equal(a, b), npieces
 
 
+@pytest.mark.parametrize("mag", [1.0, 1e-6, 3e3])
+@pytest.mark.parametrize("shape", [(2, 32, 8, 16), (4, 128, 16, 16), (2, 64, 64, 64)])
+def test_bn_backward_split_2xfp16_scale(shape, mag):
+    """bn_backward_split with npieces 2: the statistics pass bounds |dx| and picks a
+    power-of-two scale s (coef[3C]) with 2^8 <= max|dx| * s <= 2^14, so the fp16
+    pieces neither overflow nor sit in the subnormal range; the pieces carry dx * s
+    to 2^-22 of each element (dx as bn_backward computes it), whatever the
+    gradient's magnitude (mag scales dz); dgamma / dbeta as the 3-piece call's."""
+    from ubpl_amd import kernels as Kn
+    B, C, H, W = shape
+    gen = torch.Generator().manual_seed(19 + C)
+    d = lambda t: t.to(DEV)
+    dz, x = d(torch.randn(B, C, H, W, generator=gen) * mag), d(torch.randn(B, C, H, W, generator=gen))
+    gamma = d(torch.rand(C, generator=gen) + 0.5)
+    mean, istd = d(torch.randn(C, generator=gen) * 0.1), d(torch.rand(C, generator=gen) + 0.5)
+    sc, sh = gamma * istd, d(torch.randn(C, generator=gen)) - mean * gamma * istd
+    part = torch.zeros(int(__import__("ubpl_amd")._lib.lib().ubpl_bn_part_doubles(B, C)), dtype=torch.float64,
+                       device=DEV)
+    coef = torch.full((3 * C + 1,), -1.0, device=DEV)
+    dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dx = Kn.bn_backward(dz, x, gamma, mean, istd, sc, sh, 1, part, coef, dg, db, out=torch.empty_like(dz))
+    dg2, db2 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    ys = Kn.bn_backward_split(dz, x, gamma, mean, istd, sc, sh, 1, part, coef, dg2, db2, 2, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)
+    s = float(ys.scale.item())
+    m, e = np.frexp(s)
+    assert m == 0.5, s                                          # a power of two
+    amax = float(dx.abs().max())
+    assert 2.0 ** 8 <= amax * s <= 2.0 ** 14, (amax, s)
+    planes = ys.buf.view(2, ys.plane).cpu()
+    img = (planes[0].view(torch.float16).double() + planes[1].view(torch.float16).double()) / s
+    img = img.view(B, C // 16, H + 2, W + 2, 16)[:, :, 1:-1, 1:-1].permute(0, 1, 4, 2, 3).reshape(B, C, H, W)
+    ref = dx.double().cpu()
+    assert float(((img - ref).abs() - 2.0 ** -22 * ref.abs()).max()) <= 2.0 ** -26 * amax
+
+
+@pytest.mark.parametrize("case", [(2, 128, 128, 64, 64), (3, 128, 128, 16, 32), (2, 64, 64, 32, 32),
+                                  (2, 128, 128, 8, 8)])
+def test_2xfp16_3x3_gradients_vs_f64(case):
+    """The 2xfp16 backward of a 3x3 conv: dy through bn_backward_split (npieces 2, its
+    device-side scale), the data gradient on the mode-1 fp16 weights and the weight
+    gradient against the forward's fp16 image of the conv input, each within F16_BAR
+    of the exact-f32 kernels' error against float64 (dy scaled small, as real
+    gradients are)."""
+    from ubpl_amd import kernels as Kn
+    B, Cin, Cout, H, W = case
+    gen = torch.Generator().manual_seed(61 + H)
+    d = lambda t: t.to(DEV)
+    x = torch.randn(B, Cin, H, W, generator=gen)
+    w = torch.randn(Cout, Cin, 3, 3, generator=gen) / np.sqrt(Cin * 9)
+    sc, sh = torch.rand(Cin, generator=gen) + 0.5, torch.randn(Cin, generator=gen) * 0.5
+    # dy as the BN backward produces it (identity-like BN coefficients), magnitude ~1e-5
+    dz = torch.randn(B, Cout, H, W, generator=gen) * 1e-5
+    xb = torch.randn(B, Cout, H, W, generator=gen)
+    gamma = torch.rand(Cout, generator=gen) + 0.5
+    mean, istd = torch.randn(Cout, generator=gen) * 0.1, torch.rand(Cout, generator=gen) + 0.5
+    bsc, bsh = gamma * istd, torch.randn(Cout, generator=gen) - mean * gamma * istd
+    part = torch.zeros(int(__import__("ubpl_amd")._lib.lib().ubpl_bn_part_doubles(B, Cout)), dtype=torch.float64,
+                       device=DEV)
+    coef = torch.empty(3 * Cout + 1, device=DEV)
+    dg, db_ = torch.zeros(Cout, device=DEV), torch.zeros(Cout, device=DEV)
+    dy = Kn.bn_backward(d(dz), d(xb), d(gamma), d(mean), d(istd), d(bsc), d(bsh), 1, part, coef, dg, db_,
+                        out=torch.empty(B, Cout, H, W, device=DEV))
+    ys = Kn.bn_backward_split(d(dz), d(xb), d(gamma), d(mean), d(istd), d(bsc), d(bsh), 1, part, coef, None, None,
+                              2, 1)
+    dy64 = dy.double().cpu()
+    # data gradient
+    dxref = torch.nn.grad.conv2d_input((B, Cin, H, W), w.double(), dy64, 1, 1)
+    dx = Kn.conv2d_forward_psa(ys, Kn.conv_weight_split(d(w), 1, 2), None)
+    dx32 = Kn.conv2d_dgrad(dy, d(w))
+    e32, e16 = _rel(dx32, dxref), _rel(dx, dxref)
+    print("2xfp16 dgrad %s: f32 %.2e 2xfp16 %.2e" % (case, e32, e16))
+    assert e16 <= F16_BAR * e32 + 1e-8, (e16, e32)
+    # weight gradient from the forward's 2xfp16 image
+    inp = F.relu((x.double() * sc.double()[None, :, None, None] + sh.double()[None, :, None, None]).float())
+    dwref = torch.nn.grad.conv2d_weight(inp.double(), (Cout, Cin, 3, 3), dy64, 1, 1)
+    xs = Kn.split_activation(d(x), 2, 1, d(sc), d(sh))
+    if Kn.wgrad3_psa_ok(ys, xs):
+        dw, dbw = torch.zeros(Cout, Cin, 3, 3, device=DEV), torch.zeros(Cout, device=DEV)
+        Kn.conv2d_wgrad3_psa(ys, xs, dw, dbw, accumulate=False)
+        dw32, db32 = torch.zeros(Cout, Cin, 3, 3, device=DEV), torch.zeros(Cout, device=DEV)
+        Kn.conv2d_wgrad(dy, d(x), 3, 1, dw32, db32, d(sc), d(sh), accumulate=False)
+        e32, e16 = _rel(dw32, dwref), _rel(dw, dwref)
+        print("2xfp16 wgrad %s: f32 %.2e 2xfp16 %.2e" % (case, e32, e16))
+        assert e16 <= F16_BAR * e32 + 1e-8, (e16, e32)
+        assert _rel(dbw, dy64.sum((0, 2, 3))) <= 1e-5
+
+
 # (B, Cin, H, Cout, prologue, residual): 128- and 64-row tiles, a pixel tail
 # (N % 256 != 0) and 256-pixel tiles spanning several images (P < 256)
 SOL_CASES = [

@@ -89,6 +89,47 @@ __device__ __forceinline__ bool combine_slices(double* pc, int sp, int nsp, unsi
     return lane == 0;
 }
 
+// The same hand-off with 4 values per slice: (S1, S2) summed in a fixed order and
+// (Mg, Mx) maxima (order-free): the bounded backward statistics (bwd_stats_kernel
+// BOUND).  Channel stride chan_stride(2 * nsp).  Returns true in EVERY lane of wave 0
+// of the channel's last block (wave-uniform), the totals in lane 0.
+__device__ __forceinline__ bool combine_slices4(double* pc, int sp, int nsp, unsigned* cnt, double d1, double d2,
+                                                float m1, float m2, double& t1, double& t2, float& u1, float& u2) {
+    if (threadIdx.x >= 64) return false;
+    const int lane = threadIdx.x;
+    int last = 0;
+    if (lane == 0) {
+        publish2(pc + sp * 4, d1, d2);
+        publish2(pc + sp * 4 + 2, (double)m1, (double)m2);
+        last = last_arriver(cnt, nsp) ? 1 : 0;
+    }
+    if (!__shfl(last, 0, 64)) return false;
+    t1 = 0.0;
+    t2 = 0.0;
+    double a1 = 0.0, a2 = 0.0;
+    for (int q = lane; q < nsp; q += 64) {
+        t1 += consume(pc + q * 4);
+        t2 += consume(pc + q * 4 + 1);
+        a1 = fmax(a1, consume(pc + q * 4 + 2));
+        a2 = fmax(a2, consume(pc + q * 4 + 3));
+    }
+    t1 = ubpl::wave_sum(t1);
+    t2 = ubpl::wave_sum(t2);
+    u1 = ubpl::wave_max((float)a1);
+    u2 = ubpl::wave_max((float)a2);
+    return true;
+}
+
+// Power-of-two scale that puts a tensor whose |values| <= bound at <= 2^14 (the
+// 2xfp16 split's operand range: common.h split2); 1 for an all-zero tensor.
+__device__ __forceinline__ float fp16_scale_for(float bound) {
+    if (!(bound > 0.f) || !isfinite(bound)) return 1.f;
+    int e;
+    frexpf(bound, &e);                     // bound < 2^e
+    e = min(max(14 - e, -60), 60);
+    return ldexpf(1.f, e);
+}
+
 struct StatsOut {
     const float* gamma;
     const float* beta;
@@ -237,12 +278,17 @@ struct BwdOut {
     const float* gamma;
     const float* invstd;
     float *dgamma, *dbeta, *ca, *cb, *cc;
+    // BOUND: per channel a bound of |dx| (|a| max|g| + |b| max|x - mean| + |c|) into bnd[c],
+    // and from the tensor's last channel the 2xfp16 scale of dx (fp16_scale_for) into *dxscale
+    float* bnd;
+    unsigned* tcnt;
+    float* dxscale;
 };
 
 // Per (channel, slice): S1 = sum dyp, S2 = sum dyp*(x - mean) with the ReLU
 // mask recomputed; the channel's last block produces dgamma/dbeta and the
 // coefficients of dx = a*dyp + b*(x - mean) + c.
-template <bool VEC>
+template <bool VEC, bool BOUND = false>
 __global__ void __launch_bounds__(256) bwd_stats_kernel(const float* __restrict__ dz, const float* __restrict__ x,
                                                        int B, int C, int HW, int bper,
                                                        const float* __restrict__ scale,
@@ -251,10 +297,12 @@ __global__ void __launch_bounds__(256) bwd_stats_kernel(const float* __restrict_
                                                        double* __restrict__ part, unsigned* __restrict__ cnt,
                                                        BwdOut o) {
     __shared__ double red[16];
+    __shared__ float redf[16];
     const int c = blockIdx.x, sp = blockIdx.y;
     const int b0 = sp * bper, b1 = min(B, b0 + bper);
     const float sc = scale[c], sh = shift[c], mu = mean[c];
     float s1 = 0.f, s2 = 0.f;
+    float mg = 0.f, mx = 0.f;   // BOUND: max |g|, max |x - mean| of the slice
     if (VEC) {
         // (visit_chan4 here measured 7 % slower: the flattened loop stays; on the small
         // planes — <= 8 iterations per thread — all of them load first, then accumulate
@@ -272,6 +320,11 @@ __global__ void __launch_bounds__(256) bwd_stats_kernel(const float* __restrict_
             }
             s1 += (g.x + g.y) + (g.z + g.w);
             s2 = fmaf(g.x, xv.x - mu, fmaf(g.y, xv.y - mu, fmaf(g.z, xv.z - mu, fmaf(g.w, xv.w - mu, s2))));
+            if (BOUND) {
+                mg = fmaxf(mg, fmaxf(fmaxf(fabsf(g.x), fabsf(g.y)), fmaxf(fabsf(g.z), fabsf(g.w))));
+                mx = fmaxf(mx, fmaxf(fmaxf(fabsf(xv.x - mu), fabsf(xv.y - mu)),
+                                     fmaxf(fabsf(xv.z - mu), fabsf(xv.w - mu))));
+            }
         };
         auto off_of = [&](int i) {
             const int bb = i / hw4, o4 = i - bb * hw4;
@@ -308,19 +361,59 @@ __global__ void __launch_bounds__(256) bwd_stats_kernel(const float* __restrict_
             if (relu && !(fmaf(xv, sc, sh) > 0.f)) g = 0.f;
             s1 += g;
             s2 = fmaf(g, xv - mu, s2);
+            if (BOUND) {
+                mg = fmaxf(mg, fabsf(g));
+                mx = fmaxf(mx, fabsf(xv - mu));
+            }
         }
     }
     const double d1 = ubpl::block_sum((double)s1, red);
     const double d2 = ubpl::block_sum((double)s2, red);
     double t1, t2;
-    if (!combine_slices(part + (int64_t)c * chan_stride(gridDim.y), sp, gridDim.y, cnt + c, d1, d2, t1, t2)) return;
-    const double N = (double)((int64_t)B * HW);
-    const double is = o.invstd[c], g = o.gamma[c];
-    if (o.dgamma) o.dgamma[c] += (float)(t2 * is);
-    if (o.dbeta) o.dbeta[c] += (float)t1;
-    o.ca[c] = (float)(g * is);
-    o.cb[c] = (float)(-g * is * is * is * t2 / N);
-    o.cc[c] = (float)(-g * is * t1 / N);
+    if constexpr (!BOUND) {
+        if (!combine_slices(part + (int64_t)c * chan_stride(gridDim.y), sp, gridDim.y, cnt + c, d1, d2, t1, t2))
+            return;
+        const double N = (double)((int64_t)B * HW);
+        const double is = o.invstd[c], g = o.gamma[c];
+        if (o.dgamma) o.dgamma[c] += (float)(t2 * is);
+        if (o.dbeta) o.dbeta[c] += (float)t1;
+        o.ca[c] = (float)(g * is);
+        o.cb[c] = (float)(-g * is * is * is * t2 / N);
+        o.cc[c] = (float)(-g * is * t1 / N);
+    } else {
+        const float bmg = ubpl::block_max(mg, redf);
+        const float bmx = ubpl::block_max(mx, redf);
+        float ug, ux;
+        if (!combine_slices4(part + (int64_t)c * chan_stride(2 * gridDim.y), sp, gridDim.y, cnt + c, d1, d2, bmg,
+                             bmx, t1, t2, ug, ux))
+            return;
+        // wave 0 of the channel's last block (converged); lane 0 holds the totals
+        const int lane = threadIdx.x;
+        int tlast = 0;
+        if (lane == 0) {
+            const double N = (double)((int64_t)B * HW);
+            const double is = o.invstd[c], g = o.gamma[c];
+            if (o.dgamma) o.dgamma[c] += (float)(t2 * is);
+            if (o.dbeta) o.dbeta[c] += (float)t1;
+            const float a = (float)(g * is), bq = (float)(-g * is * is * is * t2 / N), cq = (float)(-g * is * t1 / N);
+            o.ca[c] = a;
+            o.cb[c] = bq;
+            o.cc[c] = cq;
+            // |dx| <= |a| max|g| + |b| max|x - mean| + |c|, 1 % over for the f32 rounding of dx
+            const float bound = 1.01f * (fabsf(a) * ug + fabsf(bq) * ux + fabsf(cq));
+            __hip_atomic_store(reinterpret_cast<unsigned*>(o.bnd + c), __float_as_uint(bound), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            tlast = last_arriver(o.tcnt, C) ? 1 : 0;
+        }
+        if (!__shfl(tlast, 0, 64)) return;
+        // the tensor's last channel: max over every channel's bound -> the scale of dx
+        float m = 0.f;
+        for (int q = lane; q < C; q += 64)
+            m = fmaxf(m, __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(o.bnd + q),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+        m = ubpl::wave_max(m);
+        if (lane == 0) *o.dxscale = fp16_scale_for(m);
+    }
 }
 
 // Backward statistics partials, per (channel c, 64-pixel slice q of the flat
@@ -557,6 +650,7 @@ int grid_ew(int64_t n) {
 // 2 * splits partial sums, channels chan_stride(splits) doubles apart.
 constexpr int MAXBN = 512;
 constexpr int CNT_DOUBLES = MAXBN / 2;
+constexpr int MAX_SPLITS = 2048 / 64 + 1;   // splits_for's bound for C >= 64 (and B)
 // ---- statistics from 64-pixel partials (conv-epilogue fused: common.h
 // tile_bn_partials; or bn_partials_kernel below).  part [C][np][2] f32 =
 // (S, M2) per slice, Chan's parallel form.
@@ -683,7 +777,13 @@ UBPL_API int ubpl_bn_stats_from_partials(const float* part, int C, int64_t N, co
     UBPL_LAUNCH_CHECK();
     return 0;
 }
-UBPL_API int64_t ubpl_bn_part_doubles(int B, int C) { return CNT_DOUBLES + (int64_t)C * chan_stride(splits_for(B, C)); }
+// (+ the bounded backward statistics' area: 4 doubles per slice of up to MAXBN channels, then a
+// tensor ticket and MAXBN per-channel bounds; the tickets return to zero after every launch)
+UBPL_API int64_t ubpl_bn_part_doubles(int B, int C) {
+    (void)B;
+    (void)C;
+    return CNT_DOUBLES + (int64_t)MAXBN * chan_stride(2 * MAX_SPLITS) + 32 + MAXBN / 2;
+}
 
 // Train-mode statistics of x [B,C,H,W] -> mean, invstd, (scale, shift) and the
 // running-stat update (rmean/rvar nullable: track_running_stats off).
@@ -747,7 +847,9 @@ __global__ void __launch_bounds__(256) bwd_apply_split_kernel(const float* __res
                                                              const float* __restrict__ ca,
                                                              const float* __restrict__ cb,
                                                              const float* __restrict__ cc, int pad,
-                                                             uint16_t* __restrict__ dst, int64_t plane) {
+                                                             uint16_t* __restrict__ dst, int64_t plane,
+                                                             const float* __restrict__ dxscale) {
+    // NP = 2 (2xfp16): the pieces of dx * (*dxscale), the power of two the statistics chose
     const int Hp = H + 2 * pad, Wp = W + 2 * pad, G = C >> 4;
     const int b = blockIdx.z, g = blockIdx.y;
     const int pix = blockIdx.x * 256 + threadIdx.x;
@@ -764,7 +866,8 @@ __global__ void __launch_bounds__(256) bwd_apply_split_kernel(const float* __res
         const float r = bwd_one(dz[o + j * HW], x[o + j * HW], scale[c], shift[c], mean[c], ca[c], cb[c], cc[c], relu);
         v[j] = in ? r : 0.f;
     }
-    ubpl::store_psa_row<NP>(v, dst + (((int64_t)(b * G + g) * Hp + hp) * Wp + wq) * 16, plane);
+    ubpl::store_psa_row<NP>(v, dst + (((int64_t)(b * G + g) * Hp + hp) * Wp + wq) * 16, plane,
+                            NP == 2 ? *dxscale : 1.f);
 }
 
 namespace {
@@ -772,15 +875,37 @@ namespace {
 // the producer's epilogue wrote the partials) the f64 finalize
 int bwd_stats(const float* dz, const float* x, int B, int C, int HW, const float* gamma, const float* mean,
               const float* invstd, const float* scale, const float* shift, int relu, double* scratch,
-              const float* part, float* coef, float* dgamma, float* dbeta, hipStream_t st) {
-    const BwdOut o{gamma, invstd, dgamma, dbeta, coef, coef + C, coef + 2 * C};
+              const float* part, float* coef, float* dgamma, float* dbeta, hipStream_t st, bool bound = false) {
+    // bound: also the 2xfp16 scale of dx at coef[3C] (bwd_stats_kernel BOUND; coef: 3C + 1 floats, the
+    // per-channel bounds and the tensor ticket in the scratch's tail)
+    unsigned* cnt = reinterpret_cast<unsigned*>(scratch);
+    BwdOut o{gamma, invstd, dgamma, dbeta, coef, coef + C, coef + 2 * C, nullptr, nullptr, nullptr};
+    if (bound) {
+        if (part != nullptr || C > MAXBN || scratch == nullptr) return (int)hipErrorInvalidValue;
+        const int splits = splits_for(B, C, HW);
+        const int bper = (B + splits - 1) / splits;
+        const int gs = (B + bper - 1) / bper;
+        double* sl = scratch + CNT_DOUBLES;
+        double* tail = sl + (int64_t)MAXBN * chan_stride(2 * MAX_SPLITS);
+        o.tcnt = reinterpret_cast<unsigned*>(tail);
+        o.bnd = reinterpret_cast<float*>(tail + 32);
+        o.dxscale = coef + 3 * C;
+        const bool vec = (HW % 4 == 0) && ((((uintptr_t)dz | (uintptr_t)x) & 15) == 0);
+        if (vec)
+            hipLaunchKernelGGL((bwd_stats_kernel<true, true>), dim3(C, gs), dim3(256), 0, st, dz, x, B, C, HW, bper,
+                               scale, shift, mean, relu, sl, cnt, o);
+        else
+            hipLaunchKernelGGL((bwd_stats_kernel<false, true>), dim3(C, gs), dim3(256), 0, st, dz, x, B, C, HW, bper,
+                               scale, shift, mean, relu, sl, cnt, o);
+        UBPL_LAUNCH_CHECK();
+        return 0;
+    }
     if (part == nullptr) {   // one launch: slices + last-arriver combine
         if (C > MAXBN || scratch == nullptr) return (int)hipErrorInvalidValue;
         const int splits = splits_for(B, C, HW);
         const int bper = (B + splits - 1) / splits;
         const int gs = (B + bper - 1) / bper;
         const bool vec = (HW % 4 == 0) && ((((uintptr_t)dz | (uintptr_t)x) & 15) == 0);
-        unsigned* cnt = reinterpret_cast<unsigned*>(scratch);
         double* sl = scratch + CNT_DOUBLES;
         if (vec)
             hipLaunchKernelGGL(bwd_stats_kernel<true>, dim3(C, gs), dim3(256), 0, st, dz, x, B, C, HW, bper, scale,
@@ -827,21 +952,23 @@ UBPL_API int ubpl_bn_backward_split(const float* dz, const float* x, int B, int 
     const int HW = H * W;
     if (C % 16 != 0 || npieces < 1 || npieces > 3 || pad < 0) return (int)hipErrorInvalidValue;
     hipStream_t st = (hipStream_t)stream;
+    // npieces 2 (2xfp16): dx scaled by the power of two its bound asks for (coef[3C]: coef holds 3C + 1 floats)
     const int e = bwd_stats(dz, x, B, C, HW, gamma, mean, invstd, scale, shift, relu, scratch, part, coef, dgamma,
-                            dbeta, st);
+                            dbeta, st, npieces == 2);
     if (e) return e;
+    const float* dxs = coef + 3 * C;
     const float *ca = coef, *cb = coef + C, *cc = coef + 2 * C;
     const int Hp = H + 2 * pad, Wp = W + 2 * pad;
     dim3 grid((unsigned)((Hp * Wp + 255) / 256), (unsigned)(C / 16), (unsigned)B);
     if (npieces == 3)
         hipLaunchKernelGGL(bwd_apply_split_kernel<3>, grid, dim3(256), 0, st, dz, x, C, H, W, scale, shift, mean,
-                           relu, ca, cb, cc, pad, dst, plane);
+                           relu, ca, cb, cc, pad, dst, plane, dxs);
     else if (npieces == 1)
         hipLaunchKernelGGL(bwd_apply_split_kernel<1>, grid, dim3(256), 0, st, dz, x, C, H, W, scale, shift, mean,
-                           relu, ca, cb, cc, pad, dst, plane);
+                           relu, ca, cb, cc, pad, dst, plane, dxs);
     else
         hipLaunchKernelGGL(bwd_apply_split_kernel<2>, grid, dim3(256), 0, st, dz, x, C, H, W, scale, shift, mean,
-                           relu, ca, cb, cc, pad, dst, plane);
+                           relu, ca, cb, cc, pad, dst, plane, dxs);
     UBPL_LAUNCH_CHECK();
     return 0;
 }

@@ -68,6 +68,13 @@ __device__ __forceinline__ floatx16 mfma_piece(const bf16x8 a, const bf16x8 b, c
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// element e of a piece fragment as f32 (fp16 pieces for NP = 2, bf16 otherwise)
+template <int NP>
+__device__ __forceinline__ float piece_elem(const bf16x8 v, int e) {
+    if constexpr (NP == 2) return (float)__builtin_bit_cast(half8, v)[e];
+    else return (float)v[e];
+}
+
 // acc += sum over piece pairs (pa, pb), pa + pb < NP, smallest terms first
 template <int NP>
 __device__ __forceinline__ void mfma_split(floatx16& acc, const bf16x8 (&a)[NP], const bf16x8 (&b)[NP]) {
@@ -524,8 +531,12 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                                                         const float* __restrict__ bias, const float* res, float* y,
                                                         int B, int Cin, int H, int W, int pad, int Cout, int kchunk,
                                                         float* __restrict__ slab, float* __restrict__ stat_part,
-                                                        ubpl::BnBwdEpi bwd, float osc) {
-    // osc: the accumulators' scale (2xfp16: weight scale x activation scale; 1 otherwise)
+                                                        ubpl::BnBwdEpi bwd, float osc,
+                                                        const float* __restrict__ ascp) {
+    // osc: the accumulators' scale (2xfp16: weight scale x activation scale, the latter
+    // read from *ascp when the image's scale lives on the device — a data gradient's,
+    // bn.hip fp16_scale_for; 1 on the other paths)
+    if (ascp != nullptr) osc *= *ascp;
     constexpr int PADK = KS / 2;   // odd KS: centred; even KS (the stem, 4x4): taps -KS/2 .. KS/2 - 1
     constexpr int T = KS * KS;
     // waves: WGM along the output channels x 4/WGM along the pixels (64-row
@@ -766,7 +777,9 @@ template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2, int BNT1 = 256>
 __global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
-                                                        int B, int Cin, int H, int Cout, float osc) {
+                                                        int B, int Cin, int H, int Cout, float osc,
+                                                        const float* __restrict__ ascp) {
+    if (ascp != nullptr) osc *= *ascp;   // (see conv_psa_kernel)
     constexpr int BNT = BNT1 * TEAMS, R = BNT / WW, W2 = WW + 2;
     static_assert(BNT1 == 256 || (BNT1 == 192 && BM == 128), "192-pixel tiles: 128 rows");
     constexpr int NW = 4 * TEAMS;              // waves (TEAMS 4-wave teams, one 256-pixel tile each)
@@ -1289,7 +1302,9 @@ template <int NP, int CB = 128>
 __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __restrict__ dys, int64_t dplane,
                                                           const uint16_t* __restrict__ xs, int64_t xplane, int B,
                                                           int Cin, int Cout, int H, int W, int steps_per_split,
-                                                          float* __restrict__ slab) {
+                                                          float* __restrict__ slab, const float* __restrict__ dscale) {
+    // NP = 2 (2xfp16): dys are the fp16 pieces of dy * (*dscale) (bn.hip fp16_scale_for), xs of
+    // x * FP16_ACT_SCALE (the forward's image): the slab gets the products unscaled exactly.
     // CB = channel block of both tile sides (128, or 64 for the 64-channel convs:
     // wave tile 32 x 32, waves 0-1 move the operands)
     constexpr int BM = CB, TM = CB / 64, TN = CB / 64, NS = 3;
@@ -1430,7 +1445,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
 #pragma unroll
                     for (int p = 0; p < NP; ++p)
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) bsum[i] += (float)af[i][p][e];
+                        for (int e = 0; e < 8; ++e) bsum[i] += piece_elem<NP>(af[i][p], e);
             }
             floatx16 tmp[TM][TN];
 #pragma unroll
@@ -1448,6 +1463,11 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
 
     float* sl = slab + (int64_t)bz * Cout * Nt;
     const int li = lane & 31, h = lane >> 5;
+    float inv = 1.f, binv = 1.f;
+    if constexpr (NP == 2) {
+        binv = 1.f / *dscale;
+        inv = binv / ubpl::FP16_ACT_SCALE;
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int n = tap * Cin + ci0 + wn + 32 * j + li;
@@ -1456,7 +1476,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                sl[(int64_t)m * Nt + n] = acc[i][j][r];
+                sl[(int64_t)m * Nt + n] = acc[i][j][r] * inv;
             }
     }
     if (bias_wave) {
@@ -1464,7 +1484,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa_kernel(const uint16_t* __res
         for (int i = 0; i < TM; ++i) {
             // lane (r, h) summed channel wm + 32i + r over pixels 8h..8h+7 of each step
             const float v = bsum[i] + __shfl_xor(bsum[i], 32, 64);
-            if (h == 0) sl[(int64_t)(m0 + wm + 32 * i + li) * Nt + Ntot] = v;
+            if (h == 0) sl[(int64_t)(m0 + wm + 32 * i + li) * Nt + Ntot] = v * binv;
         }
     }
 }
@@ -1480,7 +1500,8 @@ template <int NP>
 __global__ void __launch_bounds__(NT, 2) wgrad3_psa64_kernel(const uint16_t* __restrict__ dys, int64_t dplane,
                                                             const uint16_t* __restrict__ xs, int64_t xplane, int B,
                                                             int Cin, int Cout, int H, int W, int steps_per_split,
-                                                            float* __restrict__ slab) {
+                                                            float* __restrict__ slab, const float* __restrict__ dscale) {
+    // NP = 2: the scales of wgrad3_psa_kernel
     constexpr int TN = 3, NS = 3;
     constexpr int PI = 4 * 512;               // piece image: 4 groups x 16 px x 32 B
     constexpr int OB = NP * PI;               // one operand image (A, or one tap of B)
@@ -1597,7 +1618,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa64_kernel(const uint16_t* __r
 #pragma unroll
             for (int p = 0; p < NP; ++p)
 #pragma unroll
-                for (int e = 0; e < 8; ++e) bsum += (float)af[p][e];
+                for (int e = 0; e < 8; ++e) bsum += piece_elem<NP>(af[p], e);
         }
         floatx16 tmp[TN];
 #pragma unroll
@@ -1610,6 +1631,11 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa64_kernel(const uint16_t* __r
 
     float* sl = slab + (int64_t)bz * Cout * Nt;
     const int li = lane & 31, h = lane >> 5;
+    float inv = 1.f, binv = 1.f;
+    if constexpr (NP == 2) {
+        binv = 1.f / *dscale;
+        inv = binv / ubpl::FP16_ACT_SCALE;
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int nb = wn / 32 + j;
@@ -1617,12 +1643,12 @@ __global__ void __launch_bounds__(NT, 2) wgrad3_psa64_kernel(const uint16_t* __r
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-            sl[(int64_t)m * Nt + n] = acc[j][r];
+            sl[(int64_t)m * Nt + n] = acc[j][r] * inv;
         }
     }
     if (bias_wave) {
         const float v = bsum + __shfl_xor(bsum, 32, 64);
-        if (h == 0) sl[(int64_t)(m0 + wm + li) * Nt + Ntot] = v;
+        if (h == 0) sl[(int64_t)(m0 + wm + li) * Nt + Ntot] = v * binv;
     }
 }
 
@@ -2192,22 +2218,26 @@ void launch_split_reduce(const float* slab, int splits, int Cout, int P, int64_t
 
 // the accumulators' scale of a split conv: 2xfp16 (NP = 2) the weight scale of its contraction
 // length x the activation scale (common.h split2), else 1
-inline float psa_osc(int np, int ktot) { return np == 2 ? ubpl::fp16_wscale(ktot) * ubpl::FP16_ACT_SCALE : 1.f; }
+// (dev_act: the activation scale is read on the device, *ascp; the host part is the weight scale)
+inline float psa_osc(int np, int ktot, bool dev_act = false) {
+    return np == 2 ? ubpl::fp16_wscale(ktot) * (dev_act ? 1.f : ubpl::FP16_ACT_SCALE) : 1.f;
+}
 
 template <int BM, int KS, int NP, int BNT, int WGM = 2, int KSUB = 1>
 int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t wplane, const float* bias,
                const float* res, float* y, int B, int Cin, int H, int W, int pad, int Cout, const Plan& pl,
-               float* slab, float* stat_part, const ubpl::BnBwdEpi& bwd, hipStream_t st) {
+               float* slab, float* stat_part, const ubpl::BnBwdEpi& bwd, hipStream_t st,
+               const float* ascp = nullptr) {
     const int64_t N = (int64_t)B * H * W;
     dim3 grid((unsigned)((N + BNT - 1) / BNT), (unsigned)((Cout + BM - 1) / BM), (unsigned)pl.splits);
     const bool split = pl.splits > 1;
     const ubpl::BnBwdEpi off{nullptr, nullptr, 0, nullptr};
-    const float osc = psa_osc(NP, Cin * KS * KS);
+    const float osc = psa_osc(NP, Cin * KS * KS, ascp != nullptr);
     if constexpr (NP != 2) {   // (epilogue partials: not on the scaled 2xfp16 accumulators)
         if (!split && (stat_part || bwd.part)) {
             hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM, true, KSUB>), grid, dim3(NT), 0, st, xs, xplane,
                                wp, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl.kchunk, nullptr, stat_part, bwd,
-                               osc);
+                               osc, ascp);
             UBPL_LAUNCH_CHECK();
             return 0;
         }
@@ -2215,7 +2245,7 @@ int launch_psa(const uint16_t* xs, int64_t xplane, const uint16_t* wp, int64_t w
     hipLaunchKernelGGL((conv_psa_kernel<BM, KS, NP, BNT, WGM, false, KSUB>), grid,
                        dim3(NT), 0, st, xs, xplane, wp, wplane,
                        bias, split ? nullptr : res, y, B, Cin, H, W, pad, Cout, pl.kchunk, split ? slab : nullptr,
-                       nullptr, off, osc);
+                       nullptr, off, osc, ascp);
     UBPL_LAUNCH_CHECK();
     if (split) {
         launch_split_reduce(slab, pl.splits, Cout, H * W, N, bias, res, y, st);
@@ -2423,7 +2453,7 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
                                      const uint16_t* wsplit, int64_t wplane, const float* bias, int Cout, int KS,
                                      const float* res, float* y, float* slab, int npieces, float* stat_part,
                                      const float* bn_x, const float* bn_coef, int bn_relu, float* bn_part,
-                                     void* stream) {
+                                     const float* act_scale, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (Cin % 16 != 0 || npieces < 1 || npieces > 3 || pad < KS / 2 || (KS != 1 && KS != 3 && KS != 4))
         return (int)hipErrorInvalidValue;
@@ -2447,14 +2477,15 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         return !(e && atoi(e) == 0);
     }();
     if (npieces == 2 && (stat_part || bwd.part)) return (int)hipErrorInvalidValue;   // (6xbf16 / bf16 only)
+    if (npieces != 2 && act_scale != nullptr) return (int)hipErrorInvalidValue;
     if (KS == 4) {   // the space-to-depth stem (ubpl_stem_s2d_split): 64-row tiles on 256 pixels
         if (pl.bm != 64 || pl.splits != 1 || (npieces != 3 && npieces != 1) || N % 256 != 0)
             return (int)hipErrorInvalidValue;
         if (npieces == 1)
             return launch_psa<64, 4, 1, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout,
-                                                pl, slab, stat_part, bwd, st);
+                                                pl, slab, stat_part, bwd, st, act_scale);
         return launch_psa<64, 4, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                            slab, stat_part, bwd, st);
+                                            slab, stat_part, bwd, st, act_scale);
     }
     // the one-piece (bf16) path: KSUB 16-k steps per stage and barrier (UBPL_PSA_KSUB1 in 1..4)
     static const int ksub1 = [] {
@@ -2466,13 +2497,13 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     do {                                                                                                           \
         switch (ksub1) {                                                                                           \
             case 2: return launch_psa<BM_, KS_, 1, 256, WGM_, 2>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, \
-                                                                   H, W, pad, Cout, pl, slab, stat_part, bwd, st); \
+                                                                   H, W, pad, Cout, pl, slab, stat_part, bwd, st, act_scale); \
             case 3: return launch_psa<BM_, KS_, 1, 256, WGM_, 3>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, \
-                                                                   H, W, pad, Cout, pl, slab, stat_part, bwd, st); \
+                                                                   H, W, pad, Cout, pl, slab, stat_part, bwd, st, act_scale); \
             case 4: return launch_psa<BM_, KS_, 1, 256, WGM_, 4>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, \
-                                                                   H, W, pad, Cout, pl, slab, stat_part, bwd, st); \
+                                                                   H, W, pad, Cout, pl, slab, stat_part, bwd, st, act_scale); \
             default: return launch_psa<BM_, KS_, 1, 256, WGM_, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin,\
-                                                                    H, W, pad, Cout, pl, slab, stat_part, bwd, st);\
+                                                                    H, W, pad, Cout, pl, slab, stat_part, bwd, st, act_scale);\
         }                                                                                                          \
     } while (0)
     // 3x3 stride-1 pad-1 on the split / bf16 paths, 128- or 64-row tiles, whole-row 256-pixel
@@ -2500,7 +2531,7 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
                           w96);
     if ((halo_mode >= 2) && KS == 3 && !halo_ok) return (int)hipErrorInvalidValue;
     const bool halo = halo_mode < 0 ? ((npieces == 1 && W <= 64) || one_buf) : halo_mode != 0;
-    const float osc = psa_osc(npieces, Cin * KS * KS);
+    const float osc = psa_osc(npieces, Cin * KS * KS, act_scale != nullptr);
     if (halo && halo_ok) {
         // two 4-wave teams per workgroup (512 pixels: one halo, one A ring for both,
         // two waves per SIMD) where the grid still fills the chip; UBPL_PSA_TEAMS=1 / 2
@@ -2514,13 +2545,13 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     do {                                                                                                            \
         if (npieces == 3)                                                                                           \
             hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 2>), grid2, dim3(2 * NT), 0, st, xs, xplane, wsplit,   \
-                               wplane, bias, res, y, B, Cin, H, Cout, osc);                                         \
+                               wplane, bias, res, y, B, Cin, H, Cout, osc, act_scale);                                         \
         else if (npieces == 2)                                                                                      \
             hipLaunchKernelGGL((conv_psah_kernel<W_, 2, BM_, 2>), grid2, dim3(2 * NT), 0, st, xs, xplane, wsplit,   \
-                               wplane, bias, res, y, B, Cin, H, Cout, osc);                                         \
+                               wplane, bias, res, y, B, Cin, H, Cout, osc, act_scale);                                         \
         else                                                                                                        \
             hipLaunchKernelGGL((conv_psah_kernel<W_, 1, BM_, 2>), grid2, dim3(2 * NT), 0, st, xs, xplane, wsplit,   \
-                               wplane, bias, res, y, B, Cin, H, Cout, osc);                                         \
+                               wplane, bias, res, y, B, Cin, H, Cout, osc, act_scale);                                         \
     } while (0)
             if (pl.bm == 128) {
                 if (W == 64) UBPL_PSAH2(64, 128);
@@ -2537,13 +2568,13 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
             const dim3 g96((unsigned)(N / 192), (unsigned)(Cout / 128));
             if (npieces == 3)
                 hipLaunchKernelGGL((conv_psah_kernel<96, 3, 128, 1, 1, 192>), g96, dim3(NT), 0, st, xs, xplane, wsplit,
-                                   wplane, bias, res, y, B, Cin, H, Cout, osc);
+                                   wplane, bias, res, y, B, Cin, H, Cout, osc, act_scale);
             else if (npieces == 2)
                 hipLaunchKernelGGL((conv_psah_kernel<96, 2, 128, 1, 1, 192>), g96, dim3(NT), 0, st, xs, xplane, wsplit,
-                                   wplane, bias, res, y, B, Cin, H, Cout, osc);
+                                   wplane, bias, res, y, B, Cin, H, Cout, osc, act_scale);
             else
                 hipLaunchKernelGGL((conv_psah_kernel<96, 1, 128, 1, 2, 192>), g96, dim3(NT), 0, st, xs, xplane, wsplit,
-                                   wplane, bias, res, y, B, Cin, H, Cout, osc);
+                                   wplane, bias, res, y, B, Cin, H, Cout, osc, act_scale);
             UBPL_LAUNCH_CHECK();
             return 0;
         }
@@ -2553,19 +2584,19 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     do {                                                                                                             \
         if (npieces == 3 && one_buf)                                                                                 \
             hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_, 1, 1>), grid, dim3(NT), 0, st, xs, xplane, wsplit,      \
-                               wplane, bias, res, y, B, Cin, H, Cout, osc);                                          \
+                               wplane, bias, res, y, B, Cin, H, Cout, osc, act_scale);                                          \
         else if (npieces == 2 && one_buf)                                                                            \
             hipLaunchKernelGGL((conv_psah_kernel<W_, 2, BM_, 1, 1>), grid, dim3(NT), 0, st, xs, xplane, wsplit,      \
-                               wplane, bias, res, y, B, Cin, H, Cout, osc);                                          \
+                               wplane, bias, res, y, B, Cin, H, Cout, osc, act_scale);                                          \
         else if (npieces == 3)                                                                                       \
             hipLaunchKernelGGL((conv_psah_kernel<W_, 3, BM_>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane,    \
-                               bias, res, y, B, Cin, H, Cout, osc);                                                  \
+                               bias, res, y, B, Cin, H, Cout, osc, act_scale);                                                  \
         else if (npieces == 2)                                                                                       \
             hipLaunchKernelGGL((conv_psah_kernel<W_, 2, BM_>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane,    \
-                               bias, res, y, B, Cin, H, Cout, osc);                                                  \
+                               bias, res, y, B, Cin, H, Cout, osc, act_scale);                                                  \
         else                                                                                                         \
             hipLaunchKernelGGL((conv_psah_kernel<W_, 1, BM_>), grid, dim3(NT), 0, st, xs, xplane, wsplit, wplane,    \
-                               bias, res, y, B, Cin, H, Cout, osc);                                                  \
+                               bias, res, y, B, Cin, H, Cout, osc, act_scale);                                                  \
     } while (0)
         if (pl.bm == 128) {
             if (W == 64) UBPL_PSAH(64, 128);
@@ -2583,10 +2614,10 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     if (bm64w && pl.bm == 64 && pl.splits == 1 && N % 256 == 0 && (KS == 3 || npieces == 1)) {
         if (npieces == 3)
             return launch_psa<64, 3, 3, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                                slab, stat_part, bwd, st);
+                                                slab, stat_part, bwd, st, act_scale);
         if (npieces == 2)
             return launch_psa<64, 3, 2, 256, 1>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                                slab, stat_part, bwd, st);
+                                                slab, stat_part, bwd, st, act_scale);
         if (KS == 3) UBPL_PSA1(64, 3, 1);
         UBPL_PSA1(64, 1, 1);
     }
@@ -2598,20 +2629,20 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
         if (npieces == 2) {
             if (KS == 3)
                 return launch_psa<128, 3, 2, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout,
-                                                  pl, slab, stat_part, bwd, st);
+                                                  pl, slab, stat_part, bwd, st, act_scale);
             return launch_psa<128, 1, 2, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                              slab, stat_part, bwd, st);
+                                              slab, stat_part, bwd, st, act_scale);
         }
         if (KS == 3) {
             return launch_psa<128, 3, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                              slab, stat_part, bwd, st);
+                                              slab, stat_part, bwd, st, act_scale);
         }
         return launch_psa<128, 1, 3, 256>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl,
-                                          slab, stat_part, bwd, st);
+                                          slab, stat_part, bwd, st, act_scale);
     }
 #define UBPL_PS(BM_, KS_, NP_) \
     return launch_psa<BM_, KS_, NP_, 128>(xs, xplane, wsplit, wplane, bias, res, y, B, Cin, H, W, pad, Cout, pl, \
-                                          slab, stat_part, bwd, st)
+                                          slab, stat_part, bwd, st, act_scale)
 #define UBPL_PS_BM(KS_, NP_)          \
     if (pl.bm == 128) UBPL_PS(128, KS_, NP_); \
     UBPL_PS(64, KS_, NP_)
@@ -2762,9 +2793,10 @@ UBPL_API int64_t ubpl_wgrad3_psa_workspace(int B, int Cin, int Cout, int H, int 
 // slab: ubpl_wgrad3_psa_workspace floats.
 UBPL_API int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t* xs, int64_t xplane, int B, int Cin,
                              int Cout, int H, int W, float* slab, float* dw, float* db, int accumulate, int npieces,
-                             void* stream) {
+                             const float* dscale, void* stream) {
     hipStream_t st = (hipStream_t)stream;
-    if (Cin % 64 || Cout % 64 || W % 16 || (npieces != 3 && npieces != 1) || slab == nullptr)
+    if (Cin % 64 || Cout % 64 || W % 16 || npieces < 1 || npieces > 3 || slab == nullptr ||
+        (npieces == 2) != (dscale != nullptr))
         return (int)hipErrorInvalidValue;
     if ((((uintptr_t)dys) & 15) || (((uintptr_t)xs) & 15) || (dplane % 8) || (xplane % 8)) return (int)hipErrorInvalidValue;
     const int splits = wgrad3_splits(B, Cin, Cout, H, W);
@@ -2775,18 +2807,24 @@ UBPL_API int ubpl_wgrad3_psa(const uint16_t* dys, int64_t dplane, const uint16_t
         dim3 grid((unsigned)(9 * (Cin / cb)), (unsigned)(Cout / cb), (unsigned)splits);
         if (npieces == 1)
             hipLaunchKernelGGL((wgrad3_psa_kernel<1, 128>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin,
-                               Cout, H, W, per, slab);
+                               Cout, H, W, per, slab, dscale);
+        else if (npieces == 2)
+            hipLaunchKernelGGL((wgrad3_psa_kernel<2, 128>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin,
+                               Cout, H, W, per, slab, dscale);
         else
             hipLaunchKernelGGL((wgrad3_psa_kernel<3, 128>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin,
-                               Cout, H, W, per, slab);
+                               Cout, H, W, per, slab, dscale);
     } else {
         dim3 grid((unsigned)(3 * (Cin / 64)), (unsigned)(Cout / 64), (unsigned)splits);
         if (npieces == 1)
             hipLaunchKernelGGL((wgrad3_psa64_kernel<1>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout,
-                               H, W, per, slab);
+                               H, W, per, slab, dscale);
+        else if (npieces == 2)
+            hipLaunchKernelGGL((wgrad3_psa64_kernel<2>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout,
+                               H, W, per, slab, dscale);
         else
             hipLaunchKernelGGL((wgrad3_psa64_kernel<3>), grid, dim3(NT), 0, st, dys, dplane, xs, xplane, B, Cin, Cout,
-                               H, W, per, slab);
+                               H, W, per, slab, dscale);
     }
     UBPL_LAUNCH_CHECK();
     return ubpl_wgrad_slab_reduce(slab, splits, Cout, Cin, 9, db != nullptr, dw, db, accumulate, stream);

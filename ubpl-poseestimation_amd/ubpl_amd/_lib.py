@@ -60,7 +60,7 @@ SIGNATURES = {
     "ubpl_conv_weights_relayout": (I, [P, P, P, I, I, P]),
     "ubpl_wgrad_slab_reduce": (I, [P, I, I, I, I, I, P, P, I, P]),
     "ubpl_wgrad3_psa_workspace": (L, [I, I, I, I, I]),
-    "ubpl_wgrad3_psa": (I, [P, L, P, L, I, I, I, I, I, P, P, P, I, I, P]),
+    "ubpl_wgrad3_psa": (I, [P, L, P, L, I, I, I, I, I, P, P, P, I, I, P, P]),
     "ubpl_wgrad_stem_psa_workspace": (L, [I, I, I, I]),
     "ubpl_wgrad_stem_psa": (I, [P, L, P, L, I, I, I, I, I, I, P, P, P, I, I, P]),
     "ubpl_wgrad1x1_split_load_workspace": (L, [I, I, I, I]),
@@ -71,7 +71,7 @@ SIGNATURES = {
     "ubpl_split_activation": (I, [P, I, I, I, I, P, P, I, I, P, L, P, L, P]),
     "ubpl_conv2d_forward_psa_workspace": (L, [I, I, I, I, I, I, I]),
     "ubpl_set_psa_dispatch": (I, [I, I]),
-    "ubpl_conv2d_forward_psa": (I, [P, L, I, I, I, I, I, P, L, P, I, I, P, P, P, I, P, P, P, I, P, P]),
+    "ubpl_conv2d_forward_psa": (I, [P, L, I, I, I, I, I, P, L, P, I, I, P, P, P, I, P, P, P, I, P, P, P]),
     "ubpl_stem_s2d_split": (I, [P, I, I, I, I, I, I, P, L, P]),
     "ubpl_stem_weight_s2d_split": (I, [P, I, I, I, I, P, L, P]),
     "ubpl_conv1x1_split_load_preferred": (I, [I, I, I, I]),

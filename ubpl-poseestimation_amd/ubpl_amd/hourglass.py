@@ -50,6 +50,10 @@ _STEM_WGRAD = os.environ.get("UBPL_STEM_WGRAD", "1") != "0"
 # epilogue partials + a finalize launch measured 1.3 % slower than the one-launch
 # statistics pass (stats_kernel) on the training step.
 _FWD_EPI = os.environ.get("UBPL_FWD_EPI", "0") == "1"
+# 2xfp16: the 3x3 data / weight gradients on 2xfp16 too (dy scaled by the BN backward's bound of
+# it, bn.hip bwd_stats_kernel BOUND); UBPL_FP16_BWD3=0: on 6xbf16 (with the forward's 6xbf16 image
+# kept for the weight gradient)
+_FP16_BWD3 = os.environ.get("UBPL_FP16_BWD3", "1") != "0"
 # diagnostic (tools/graph_fwd_probe.py locate): the hourglass upsample-add out of place, its
 # up1 input saved, so a graph replay's first wrong activation can name up1 or the add
 _UPADD_OOP = os.environ.get("UBPL_UPADD_OOP", "0") == "1"
@@ -257,7 +261,9 @@ class StackedHourglass(nn.Module):
                  split while they are staged, the rest f32;
         '2xfp16' the forward convs as '6xbf16' places them, on 2 fp16 pieces of the
                  power-of-two-scaled operands (3 MFMA products instead of 6, operands
-                 to 2^-22); the backward (data and weight gradients) on 6xbf16;
+                 to 2^-22); the 3x3 data and weight gradients too, their dy scaled
+                 by the power of two the BN backward's bound of it picks
+                 (UBPL_FP16_BWD3=0: on 6xbf16); the 1x1 gradients on 6xbf16;
         'bf16'   every conv with 16-channel contraction groups (3x3 and 1x1, forward
                  and data gradient) with ONE piece per operand = bf16 operands, f32
                  accumulation (BASELINE config 5's throughput path): 1x1 convs whose
@@ -269,6 +275,8 @@ class StackedHourglass(nn.Module):
         6xbf16 space-to-depth path."""
         self.conv_pieces = Kn.conv_precision_pieces(name)          # the forward's
         self.bwd_pieces = Kn.backward_pieces(self.conv_pieces)      # the gradients'
+        # the 3x3 convs' gradients (data and weight) on the forward's 2xfp16 too
+        self.bwd3_pieces = 2 if self.conv_pieces == 2 and _FP16_BWD3 else self.bwd_pieces
         self._build_weight_tables()
 
     def _build_weight_tables(self):
@@ -280,29 +288,38 @@ class StackedHourglass(nn.Module):
         stem = "pre.0.conv.weight"
         self._wsp = {}
         for mode in (0, 1):
-            pieces = self.conv_pieces if mode == 0 else self.bwd_pieces
-            rows, idx, o = [], {}, 0
+            # the pieces of a conv's table: the forward's (mode 0), its gradients' (mode 1: 3x3
+            # and 1x1 may differ under 2xfp16) — one batched split launch per piece count
+            pieces_of = (lambda ks: self.conv_pieces) if mode == 0 else \
+                (lambda ks: self.bwd3_pieces if ks == 3 else self.bwd_pieces)
+            tables = {}
             for name, shape, kind, live in tab:
+                pieces = pieces_of(shape[2])
                 if kind != "cw" or not live or name == stem or not pieces or shape[1 if mode == 0 else 0] % 16:
                     continue
                 # 6xbf16 / 2xfp16: 3x3 (PSA path) and 1x1 (split on load; outputs of 16 channels
                 # and up, the heatmap projection included)
                 if pieces in (2, 3) and not (shape[2] == 3 or (shape[2] == 1 and shape[0 if mode == 0 else 1] % 16 == 0)):
                     continue
+                rows, idx, o = tables.setdefault(pieces, ([], {}, [0]))
                 s, n, _ = offs[name]
                 T = shape[2] * shape[3]
-                rows.append((s, o, shape[0], shape[1], T))
-                idx[name] = (o, (shape[0], T, shape[1]) if mode == 0 else (shape[1], T, shape[0]))
-                o += (n + 7) // 8 * 8
-            buf = torch.empty(max(pieces, 1) * max(o, 8), dtype=torch.int16, device=device)
-            self._wsp[mode] = [torch.tensor(rows, dtype=torch.int64).reshape(-1, 5).to(device), max(o, 8), idx, buf,
-                               pieces]
+                rows.append((s, o[0], shape[0], shape[1], T))
+                idx[name] = (o[0], (shape[0], T, shape[1]) if mode == 0 else (shape[1], T, shape[0]))
+                o[0] += (n + 7) // 8 * 8
+            subs = []
+            for pieces, (rows, idx, o) in sorted(tables.items()):
+                buf = torch.empty(max(pieces, 1) * max(o[0], 8), dtype=torch.int16, device=device)
+                subs.append([torch.tensor(rows, dtype=torch.int64).reshape(-1, 5).to(device), max(o[0], 8), idx, buf,
+                             pieces])
+            self._wsp[mode] = subs
         self._wlay = {}
         for mode in (0, 1):
             need = (lambda ks, nm: ks > 1) if mode == 0 else (lambda ks, nm: nm != stem)
             # (1x1 convs stay in "rest" too: the f32 kernel takes the small planes)
-            for key, keep in ((mode, need), (("rest", mode), lambda ks, nm, m=mode, f=need:
-                                               f(ks, nm) and (ks == 1 or nm not in self._wsp[m][2]))):
+            on_split = set(nm for sub in self._wsp[mode] for nm in sub[2])
+            for key, keep in ((mode, need), (("rest", mode), lambda ks, nm, f=need, sp=on_split:
+                                               f(ks, nm) and (ks == 1 or nm not in sp))):
                 rows, idx, o = [], {}, 0
                 for name, shape, kind, live in tab:
                     if kind != "cw" or not live or not keep(shape[2], name):
@@ -317,8 +334,8 @@ class StackedHourglass(nn.Module):
 
     def relayout_weights(self, mode):
         if self.conv_pieces:
-            tbl, plane, _, buf, pieces = self._wsp[mode]
-            Kn.conv_weights_split(self.flat_params, buf, plane, tbl, mode, pieces)
+            for tbl, plane, _, buf, pieces in self._wsp[mode]:
+                Kn.conv_weights_split(self.flat_params, buf, plane, tbl, mode, pieces)
             tbl, buf, _, m = self._wlay[("rest", mode)]
             if tbl.shape[0]:
                 Kn.conv_weights_relayout(self.flat_params, buf, tbl, m)
@@ -333,12 +350,14 @@ class StackedHourglass(nn.Module):
         return buf[o:o + shp[0] * shp[1] * shp[2]].view(shp)
 
     def SW(self, mode, name):
-        """Split-bf16 weights of a conv (None when it is not on the split path)."""
-        _, plane, idx, buf, pieces = self._wsp[mode]
-        if not self.conv_pieces or name not in idx:
+        """Split weights of a conv (None when it is not on the split path)."""
+        if not self.conv_pieces:
             return None
-        o, shp = idx[name]
-        return Kn.SplitWeights(buf, plane, o, shp, pieces)
+        for _, plane, idx, buf, pieces in self._wsp[mode]:
+            if name in idx:
+                o, shp = idx[name]
+                return Kn.SplitWeights(buf, plane, o, shp, pieces)
+        return None
 
     def alt_grad_buffer(self):
         """Second gradient buffer for a backward pass that runs concurrently with
@@ -421,7 +440,7 @@ class StackedHourglass(nn.Module):
                 n = max(n, int(_lib.lib().ubpl_bn_part_doubles(B, c)))
             # zeroed once: the arrival counters at its tail reset themselves
             self._ws[key] = torch.zeros(n, dtype=torch.float64, device=self.flat_params.device)
-            self._ws[("coef", B)] = torch.empty(3 * 512, device=self.flat_params.device)
+            self._ws[("coef", B)] = torch.empty(3 * 512 + 4, device=self.flat_params.device)
         return self._ws[key]
 
     def _forward_impl(self, imgs, save):
@@ -534,7 +553,7 @@ class _Exec:
         if self.bwd_stream is not None:
             key = ("alt", B)
             if key not in model._ws:
-                model._ws[key] = (torch.zeros_like(part), torch.empty(3 * 512, device=dev))
+                model._ws[key] = (torch.zeros_like(part), torch.empty(3 * 512 + 4, device=dev))
             self.bpart, self.bcoef = model._ws[key]
         else:
             self.bpart, self.bcoef = part, None
@@ -621,9 +640,9 @@ class _Exec:
             if ws.npieces in (1, 2, 3):
                 part = mkpart() if ws.npieces != 2 else None
                 keep = self.do_save and ws.shape[1] == 9
-                if ws.npieces == 2 and keep:
-                    # 2xfp16: the conv's fp16 image and, from the same read, the 6xbf16 one
-                    # its weight gradient takes
+                if ws.npieces == 2 and keep and self.m.bwd3_pieces == 3:
+                    # 2xfp16 forward, 6xbf16 gradients: the conv's fp16 image and, from the same
+                    # read, the 6xbf16 one its weight gradient takes
                     xs, xs3 = Kn.split_activation(x, 2, 1, ps, ph, with3=True)
                     self.saved_split[name] = xs3
                 else:
@@ -724,11 +743,15 @@ class _Exec:
                               self.G(name + ".weight"), self.G(name + ".bias"), add1=add1, add2=add2, out=out,
                               part=part)
 
-    def bn_bwd_split(self, name, dz, x, relu, part=None):
+    def bn_bwd_split(self, name, dz, x, relu, part=None, pieces=None, grads=True):
+        """dx as the split operand (pieces: the consumer's; 2 = 2xfp16 with its device-side
+        scale); grads=False: the BN's own parameter gradients not accumulated (a second
+        pass over the same dz)."""
         sc, sh, mu, istd = self.bnc(name)
         return Kn.bn_backward_split(dz, x, self.m.P(name + ".weight"), mu, istd, sc, sh, relu, self.bpart,
-                                    self._coef(), self.G(name + ".weight"), self.G(name + ".bias"),
-                                    self.m.bwd_pieces, 1, part=part)
+                                    self._coef(), self.G(name + ".weight") if grads else None,
+                                    self.G(name + ".bias") if grads else None,
+                                    self.m.bwd_pieces if pieces is None else pieces, 1, part=None if not grads else part)
 
     def wgrad(self, name, dy, x, KS, stride=1, pro=None):
         ps, ph = (None, None) if pro is None else pro
@@ -782,18 +805,26 @@ class _Exec:
         ws = self.m.SW(1, p + ".conv2.conv.weight")
         xs = self.saved_split.get(p + ".conv2.conv")
         cb = 64 if _WGRAD3_64 else 128
-        split_wgrad = (ws is not None and ws.npieces in (1, 3) and xs is not None and t2.shape[1] % cb == 0
-                       and xs.C % cb == 0 and t2.shape[3] % 16 == 0)
+        split_wgrad = (ws is not None and ws.npieces in (1, 2, 3) and xs is not None and t2.shape[1] % cb == 0
+                       and xs.C % cb == 0 and t2.shape[3] % 16 == 0 and xs.npieces == ws.npieces)
         bwd2, part2 = self.bwd_epi(p + ".bn2", t1)
+        if ws is not None and ws.npieces == 2:
+            bwd2, part2 = None, None                                   # (no epilogue partials on 2xfp16)
         if split_wgrad:
             # d t2 only as the split operand both conv2 gradients read
-            ys = self.bn_bwd_split(p + ".bn3", d, t2, relu=1, part=part)
+            ys = self.bn_bwd_split(p + ".bn3", d, t2, relu=1, part=part, pieces=ws.npieces)
             Kn.conv2d_wgrad3_psa(ys, xs, self.G(p + ".conv2.conv.weight"), self.G(p + ".conv2.conv.bias"))
             d = Kn.conv2d_forward_psa(ys, ws, None, bwd=bwd2)         # d relu(bn2(t1))
-        elif ws is not None and ws.npieces in (1, 3):
+        elif ws is not None and ws.npieces in (1, 2, 3):
+            ys = None
+            if ws.npieces == 2:
+                # the data gradient's 2xfp16 operand with its bound-derived scale, from a second
+                # statistics pass over the same dz (the BN's parameter gradients accumulate once, below)
+                ys = self.bn_bwd_split(p + ".bn3", d, t2, relu=1, pieces=2, grads=False)
             d = self.bn_bwd(p + ".bn3", d, t2, relu=1, part=part)     # d t2
             self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)
-            d = Kn.conv2d_forward_psa(Kn.split_activation(d, ws.npieces, 1), ws, None, bwd=bwd2)
+            d = Kn.conv2d_forward_psa(ys if ys is not None else Kn.split_activation(d, ws.npieces, 1), ws, None,
+                                      bwd=bwd2)
         else:
             d = self.bn_bwd(p + ".bn3", d, t2, relu=1, part=part)     # d t2
             self.wgrad(p + ".conv2.conv", d, t1, 3, pro=c2)

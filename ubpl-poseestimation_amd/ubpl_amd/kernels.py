@@ -256,14 +256,17 @@ def bn_stats_from_partials(part, C, N, gamma, beta, eps, momentum, rmean, rvar, 
 
 def bn_backward_split(dz, x, gamma, mean, invstd, scale, shift, relu, scratch, coef, dgamma, dbeta, npieces, pad,
                       part=None):
-    """bn_backward with dx delivered as a SplitAct (PSA planes) only."""
+    """bn_backward with dx delivered as a SplitAct (PSA planes) only.  npieces 2
+    (2xfp16): the pieces of dx times the power of two its bound asks for, kept on
+    the device at coef[3C] — the SplitAct's `scale`, read by its consumers (so coef
+    must not be reused before they are enqueued: stream order)."""
     B, C, H, W = x.shape
     plane = B * C * (H + 2 * pad) * (W + 2 * pad)
     out = torch.empty(npieces * plane, device=x.device, dtype=torch.int16)
     call("ubpl_bn_backward_split", _p(dz), _p(x), B, C, H, W, _p(gamma), _p(mean), _p(invstd), _p(scale), _p(shift),
          int(relu), _p(scratch), _p(part), _p(coef), _p(dgamma), _p(dbeta), int(pad), int(npieces), _p(out),
          int(plane))
-    return SplitAct(out, plane, B, C, H, W, pad, npieces)
+    return SplitAct(out, plane, B, C, H, W, pad, npieces, coef[3 * C:3 * C + 1] if npieces == 2 else None)
 
 
 def bn_backward(dz, x, gamma, mean, invstd, scale, shift, relu, scratch, coef, dgamma, dbeta, add1=None, add2=None,
@@ -471,11 +474,14 @@ class SplitAct:
     [B][C/16][H+2pad][W+2pad][16] in an int16 buffer, planes `plane` elements apart
     (3: bf16 pieces; 2: fp16 pieces of v * 32, the 2xfp16 path; 1: bf16(v))."""
 
-    __slots__ = ("buf", "plane", "B", "C", "H", "W", "pad", "npieces")
+    __slots__ = ("buf", "plane", "B", "C", "H", "W", "pad", "npieces", "scale")
 
-    def __init__(self, buf, plane, B, C, H, W, pad, npieces):
+    def __init__(self, buf, plane, B, C, H, W, pad, npieces, scale=None):
         self.buf, self.plane, self.B, self.C, self.H, self.W = buf, plane, B, C, H, W
         self.pad, self.npieces = pad, npieces
+        # 2xfp16 images whose power-of-two scale lives on the device (a data gradient's: a
+        # one-float tensor); None: the fixed activation scale (32) or no scale
+        self.scale = scale
 
 
 def split_activation(x, npieces, pad, pscale=None, pshift=None, out=None, with3=False):
@@ -511,7 +517,7 @@ def conv2d_forward_psa(xs, ws, bias, res=None, out=None, stat_part=None, bwd=Non
     nws = _lib.lib().ubpl_conv2d_forward_psa_workspace(B, xs.C, Cout, KS, H, W, ws.npieces)
     slab = torch.empty(int(nws), device=xs.buf.device, dtype=F32) if nws > 0 else None
     call("ubpl_conv2d_forward_psa", _p(xs.buf), int(xs.plane), B, xs.C, H, W, int(xs.pad), ws.ptr(), int(ws.plane),
-         _p(bias), Cout, KS, _p(res), _p(y), _p(slab), int(ws.npieces), _p(stat_part), *_bnb(bwd))
+         _p(bias), Cout, KS, _p(res), _p(y), _p(slab), int(ws.npieces), _p(stat_part), *_bnb(bwd), _p(xs.scale))
     return y
 
 
@@ -580,7 +586,7 @@ def conv1x1_forward_split_load(x, ws, bias, pscale=None, pshift=None, res=None, 
 
 
 def wgrad3_psa_ok(ys, xs):
-    return (ys.npieces in (1, 3) and xs.npieces == ys.npieces and ys.pad == 1 and xs.pad == 1 and xs.C % 64 == 0
+    return (ys.npieces in (1, 2, 3) and xs.npieces == ys.npieces and (ys.npieces != 2 or ys.scale is not None) and ys.pad == 1 and xs.pad == 1 and xs.C % 64 == 0
             and ys.C % 64 == 0 and xs.W % 16 == 0 and (ys.B, ys.H, ys.W) == (xs.B, xs.H, xs.W))
 
 
@@ -589,7 +595,7 @@ def conv2d_wgrad3_psa(ys, xs, dw, db, accumulate=True):
     n = _lib.lib().ubpl_wgrad3_psa_workspace(xs.B, xs.C, ys.C, xs.H, xs.W)
     slab = torch.empty(int(n), device=xs.buf.device, dtype=F32)
     call("ubpl_wgrad3_psa", _p(ys.buf), int(ys.plane), _p(xs.buf), int(xs.plane), xs.B, xs.C, ys.C, xs.H, xs.W,
-         _p(slab), _p(dw), _p(db), int(accumulate), int(xs.npieces))
+         _p(slab), _p(dw), _p(db), int(accumulate), int(xs.npieces), _p(ys.scale))
 
 
 def wgrad_stem_psa_ok(ys, xs, w):
