@@ -677,7 +677,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                 af[i][p] = *reinterpret_cast<const bf16x8*>(base + p * BM * 32 + row * 32 + 16 * (h ^ ((row >> 3) & 1)));
             }
         }
-        if constexpr (NP == 3 && TN > 2) {
+        if constexpr (NP >= 2 && TN > 2) {
             // ping-pong chunks: tile q's 6-MFMA chain is issued with tile q-1's
             // 16 drain adds between its MFMAs (3 VALU slots per MFMA gap), so the
             // adds hide in the matrix pipe's gaps instead of trailing each chain
@@ -697,7 +697,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
                 prev = cur;
             }
             drain(acc[TM - 1][TN - 1], prev);
-        } else if constexpr (NP == 3) {
+        } else if constexpr (NP >= 2) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) read_b(j);
             // every tile's chunk chain first, the f32 adds after them (behind a

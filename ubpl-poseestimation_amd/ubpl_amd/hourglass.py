@@ -294,8 +294,10 @@ class StackedHourglass(nn.Module):
                 (lambda ks: self.bwd3_pieces if ks == 3 else self.bwd_pieces)
             tables = {}
             for name, shape, kind, live in tab:
+                if kind != "cw" or not live or name == stem:
+                    continue
                 pieces = pieces_of(shape[2])
-                if kind != "cw" or not live or name == stem or not pieces or shape[1 if mode == 0 else 0] % 16:
+                if not pieces or shape[1 if mode == 0 else 0] % 16:
                     continue
                 # 6xbf16 / 2xfp16: 3x3 (PSA path) and 1x1 (split on load; outputs of 16 channels
                 # and up, the heatmap projection included)
