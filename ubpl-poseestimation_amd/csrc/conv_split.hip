@@ -774,7 +774,7 @@ __global__ void __launch_bounds__(NT, 2) conv_psa_kernel(const uint16_t* __restr
 // BNT1: pixels per team tile — 256, or 192 for the 96-wide planes (two rows; 128-row
 // tiles only: wave tile 64 x 96, three 32-pixel fragments)
 template <int WW, int NP, int BM, int TEAMS = 1, int NHB = 2, int BNT1 = 256>
-__global__ void __launch_bounds__(NT * TEAMS, NHB == 1 ? 2 : 1) conv_psah_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
+__global__ void __launch_bounds__(NT * TEAMS, (NHB == 1 || (NP == 2 && TEAMS == 1)) ? 2 : 1) conv_psah_kernel(const uint16_t* __restrict__ xs, int64_t xplane,
                                                         const uint16_t* __restrict__ wp, int64_t wplane,
                                                         const float* __restrict__ bias, const float* res, float* y,
                                                         int B, int Cin, int H, int Cout, float osc,
@@ -2521,6 +2521,8 @@ UBPL_API int ubpl_conv2d_forward_psa(const uint16_t* xs, int64_t xplane, int B, 
     // the same order, bit for bit.
     const int halo_mode = psa_dispatch().halo;
     const bool split_np = npieces == 3 || npieces == 2;
+    // (2xfp16 on double-buffered halos at two workgroups per CU — they fit 80 KB at W <= 64 —
+    // measured slower than the one buffer: 122.4 vs 116.2 us, 426.5 vs 433.0 img/s, round 6)
     const bool one_buf = split_np && (halo_mode >= 3 || halo_mode < 0);
     // the 96-wide planes: 192-pixel tiles on 128 rows whatever the plan's row block (its
     // cost model is conv_psa_kernel's), the one-buffer variant only
