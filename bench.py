@@ -107,7 +107,7 @@ CONFIGS = {
                          desc="configs[3]: DualPose_UBPL, dual HG4, K=17, 256x256, B=16/GPU"),
     "mt_ubpl_hg8_384": dict(project="MT_UBPL", S=8, K=16, B=16, res=384,
                             desc="configs[4]: MT_UBPL, HG8, 384x384 input / 96x96 heatmaps, B=16/GPU "
-                                 "(fp32-equivalent 6xbf16 convs, not the bf16 path)"),
+                                 "(fp32-grade split convs, the headline's precision; not the bf16 path)"),
     "mt_ubpl_hg8_384_bf16": dict(project="MT_UBPL", S=8, K=16, B=16, res=384, precision="bf16",
                                  desc="configs[4]: MT_UBPL, HG8, 384x384 input / 96x96 heatmaps, B=16/GPU, "
                                       "bf16 MFMA path (conv operands bf16, f32 accumulation)"),

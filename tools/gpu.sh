@@ -11,8 +11,9 @@
 #                           $STEPS timed steps (20), $WARM warm-up (3), the CPU baseline only with CPU=1
 #     prof:<cfg>[:ENV=V,...]   rocprofv3 --kernel-trace --stats of a 3-step bench run, then
 #                           tools/prof_summary.py over its timed window -> gpurun_out/prof_<cfg>.txt
+#                           (labelled with the profiled/benched ms ratio when bench:<cfg> ran first)
 #     pmc:bench             FETCH_SIZE / WRITE_SIZE passes over the bench (eager step) ->
-#                           gpurun_out/pmc_roofline_psah.json (tools/pmc_roofline.py)
+#                           gpurun_out/pmc_roofline_$PMC_KIND.json (tools/pmc_roofline.py; psah2 default)
 #     pmc:<script.py>       SQ instruction / wait counters (one pass) + FETCH / WRITE (one pass each)
 #                           over a microbenchmark script -> gpurun_out/pmc_<name>/
 #     ab:<ENV=a>|<ENV=b>[|...]  the bench under each setting, $AB_ROUNDS rounds (2), interleaved
@@ -57,7 +58,7 @@ for step in "$@"; do
           > gpurun_out/prof_$tag.json 2> gpurun_out/prof_$tag.err
       rc=$?; [ $rc -ne 0 ] && { tail -5 gpurun_out/prof_$tag.err; stop prof $rc; }
       tr=$(find gpurun_out/prof_$tag -name "*kernel_trace.csv" | head -1)
-      python tools/prof_summary.py "$tr" 3 30 > gpurun_out/prof_$tag.txt && head -12 gpurun_out/prof_$tag.txt
+      python tools/prof_summary.py "$tr" 3 30 gpurun_out/bench_$tag.json > gpurun_out/prof_$tag.txt && head -12 gpurun_out/prof_$tag.txt
       python tools/trace_roofline.py "$tr" > gpurun_out/prof_${tag}_roofline.json 2>/dev/null || true
       find gpurun_out/prof_$tag -name "*kernel_trace.csv" -size +20M -delete ;;
     pmc)
@@ -69,8 +70,8 @@ for step in "$@"; do
               python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/$n.log 2>&1
           rc=$?; echo "pmc $n rc=$rc"; [ $rc -ne 0 ] && stop pmc $rc
         done
-        python3 tools/pmc_roofline.py $OUT gpurun_out/pmc_roofline_psah.json \
-            "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 2 --warmup 1 (eager step; tools/gpu.sh pmc:bench)" psah
+        python3 tools/pmc_roofline.py $OUT gpurun_out/pmc_roofline_${PMC_KIND:-psah2}.json \
+            "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 2 --warmup 1 (eager step; tools/gpu.sh pmc:bench)" ${PMC_KIND:-psah2}
         rm -f $OUT/*.csv
       else
         # pmc:<script.py>[:ENV=V,...]: the script's environment (the program after -- stays python3)

@@ -22,9 +22,10 @@ import sys
 
 PATS = {"f32": re.compile(r"conv_fwd_kernel<(\d+), 128, 3, 1, true, false"),
         "psa": re.compile(r"conv_psa_kernel<128, 3, 3, 256, 2(, false)?>"),
-        "psah": re.compile(r"conv_psah_kernel<64, 3, 128, 1, 1(, 256(, false)*)?>")}
+        "psah": re.compile(r"conv_psah_kernel<64, 3, 128, 1, 1(, 256(, false)*)?>"),
+        "psah2": re.compile(r"conv_psah_kernel<64, 2, 128, 1, 1(, 256)?>")}
 # psa / psah: only the 512-workgroup launches (grid size in work-items)
-GRID = {"psa": 512 * 256, "psah": 512 * 256}
+GRID = {"psa": 512 * 256, "psah": 512 * 256, "psah2": 512 * 256}
 PAT = PATS["f32"]
 KIND = "f32"
 
@@ -56,7 +57,9 @@ def main():
                       "psa": "conv_psa_kernel<128, 3, 3, 256, 2> on 512-workgroup grids (3x3 128->128 at 64x64, "
                              "B=32: forward + data gradient)",
                       "psah": "conv_psah_kernel<64, 3, 128, 1, 1, 256> on 512-workgroup grids (3x3 128->128 at "
-                              "64x64, B=32: forward + data gradient)"}[kind],
+                              "64x64, B=32: forward + data gradient)",
+                      "psah2": "conv_psah_kernel<64, 2, 128, 1, 1, 256> on 512-workgroup grids (3x3 128->128 at "
+                               "64x64, B=32, 2xfp16: forward + data gradient)"}[kind],
            "launches_fetch_pass": nf, "launches_write_pass": nw,
            "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
            "hbm_bytes_per_launch": fb + wb,

@@ -1,6 +1,11 @@
 """Summarise a rocprofv3 kernel trace of bench.py: per-kernel totals per step and per-shape conv times.
 
-    python tools/prof_summary.py <kernel_trace.csv> <timed steps> [top shapes]
+    python tools/prof_summary.py <kernel_trace.csv> <timed steps> [top shapes] [bench.json]
+
+With a bench.json (the same config benched WITHOUT the profiler) the window line
+also carries the profiled / benched ms-per-step ratio: rocprofv3's kernel trace
+serialises the captured graph's launches, so the profiled step is slower than
+the benched one and the per-kernel times are to be read with that ratio.
 
 bench.py launches a ~1-cycle spin_kernel (torch.cuda._sleep(1)) right before and
 right after its timed region; only the kernels that START between those two
@@ -9,6 +14,7 @@ replay or its 20M-cycle spin).  A trace without the markers (an older bench or
 another program) is summarised whole, and the output says so."""
 import collections
 import csv
+import json
 import re
 import sys
 
@@ -30,12 +36,22 @@ def main():
     path = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    benched = None
+    if len(sys.argv) > 4:
+        try:
+            benched = float(json.load(open(sys.argv[4]))["ms_per_step"])
+        except (OSError, ValueError, KeyError):
+            benched = None
     rows = list(csv.DictReader(open(path)))
     w = window(rows)
     if w:
         rows = [r for r in rows if w[0] <= int(r["Start_Timestamp"]) < w[1] and "spin_kernel" not in r["Kernel_Name"]]
         print("window: %d kernels between the bench's markers, %.2f ms wall (%d timed steps: %.2f ms/step)"
               % (len(rows), (w[1] - w[0]) / 1e6, steps, (w[1] - w[0]) / 1e6 / steps))
+        if benched:
+            prof = (w[1] - w[0]) / 1e6 / steps
+            print("profiled %.2f ms/step vs benched %.2f ms/step (%s): ratio %.3f"
+                  % (prof, benched, sys.argv[4], prof / benched))
     else:
         print("window: no bench markers found - the WHOLE trace is summarised")
     g = collections.defaultdict(list)
