@@ -41,6 +41,29 @@ def per_launch(path, counter):
     return vals
 
 
+def step_totals(path, counter, steps, scale):
+    """Bytes per timed step by kernel family: the dispatches between bench.py's two
+    spin-kernel markers (torch.cuda._sleep around the timed region), / steps."""
+    rows = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter and "spin_kernel" not in r["Kernel_Name"]:
+            continue
+        i = int(r["Dispatch_Id"])
+        name, v = r["Kernel_Name"], float(r["Counter_Value"]) if r["Counter_Name"] == counter else 0.0
+        rows[i] = (name, rows.get(i, (name, 0.0))[1] + v)
+    order = sorted(rows)
+    marks = [i for i in order if "spin_kernel" in rows[i][0]]
+    if len(marks) < 2:
+        return None
+    fam = {}
+    for i in order:
+        if marks[0] < i < marks[1]:
+            m = re.search(r"(\w+)(<|\()", rows[i][0].split("::")[-1])
+            k = m.group(1) if m else rows[i][0][:40]
+            fam[k] = fam.get(k, 0.0) + scale * rows[i][1] / steps
+    return fam
+
+
 def main():
     d = sys.argv[1]
     out = sys.argv[2]
@@ -65,6 +88,15 @@ def main():
            "hbm_bytes_per_launch": fb + wb,
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over bench.py; FETCH_SIZE x2 (gfx950)",
            "source": tag}
+    steps = int(os.environ.get("PMC_STEPS", "2"))
+    ft = step_totals(os.path.join(d, "fetch_counter_collection.csv"), "FETCH_SIZE", steps, 2 * 1024)
+    wt = step_totals(os.path.join(d, "write_counter_collection.csv"), "WRITE_SIZE", steps, 1024)
+    if ft and wt:
+        fams = sorted(set(ft) | set(wt), key=lambda k: -(ft.get(k, 0) + wt.get(k, 0)))
+        res["step_bytes"] = {"fetch_gb": sum(ft.values()) / 1e9, "write_gb": sum(wt.values()) / 1e9,
+                             "steps": steps, "note": "eager step: dispatches between the bench's timed-region markers",
+                             "by_kernel_gb": {k: [round(ft.get(k, 0) / 1e9, 3), round(wt.get(k, 0) / 1e9, 3)]
+                                              for k in fams[:30]}}
     print(json.dumps(res, indent=1))
     with open(out, "w") as fh:
         fh.write(json.dumps(res, indent=1) + "\n")
