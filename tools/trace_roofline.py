@@ -10,7 +10,8 @@ import os
 import json
 import sys
 
-KERNEL = os.environ.get("ROOF_KERNEL", "conv_psah_kernel<64, 3, 128, 1, 1, 256")
+# the 2xfp16 default instantiation (ROOF_KERNEL="conv_psah_kernel<64, 3, 128, 1, 1, 256" on 6xbf16)
+KERNEL = os.environ.get("ROOF_KERNEL", "conv_psah_kernel<64, 2, 128, 1, 1, 256")
 
 
 def main(path, n=60, reps=10):
