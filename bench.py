@@ -47,7 +47,12 @@ def piece_peak(npieces):
     return {3: SPLIT6_PEAK_TFLOPS, 2: SPLIT3_PEAK_TFLOPS, 1: BF16_PEAK_TFLOPS}.get(npieces, F32_MFMA_PEAK_TFLOPS)
 
 
+_KS_ONLY = [None]     # (forward_flops(..., ks=3): the 3x3 convs' share alone)
+
+
 def _conv(cin, cout, ks, hw):
+    if _KS_ONLY[0] is not None and ks != _KS_ONLY[0]:
+        return 0
     return 2 * cin * cout * ks * ks * hw * hw
 
 
@@ -62,11 +67,19 @@ def _hourglass(n, hw):
     return f + (_hourglass(n - 1, hw // 2) if n > 1 else _residual(256, 256, hw // 2))
 
 
-def forward_flops(S, K, res):
+def forward_flops(S, K, res, ks=None):
     """Conv FLOP of one StackedHourglass forward per sample (models/pose/hourglass.py:12-99,
     models/base/layers.py:53-111): 16.67 GF at HG2 256^2 K=16 — SURVEY.md §8d's 266.7 GF per
     training sample = 16 forward-equivalents (2 students x 2 views x fwd + 2 bwd, 2 teachers x
-    2 views x fwd)."""
+    2 views x fwd).  ks: only the convs of that kernel size."""
+    _KS_ONLY[0] = ks
+    try:
+        return _forward_flops(S, K, res)
+    finally:
+        _KS_ONLY[0] = None
+
+
+def _forward_flops(S, K, res):
     r2, r4 = res // 2, res // 4
     f = _conv(3, 64, 7, r2) + _residual(64, 128, r2) + _residual(128, 128, r4) + _residual(128, 256, r4)
     f += S * (_hourglass(4, r4) + _residual(256, 256, r4) + _conv(256, 256, 1, r4) + _conv(256, K, 1, r4))
@@ -77,13 +90,16 @@ def step_record(cfg, B, ms_per_step, precision):
     """Step-level fraction of the matrix peak: the step's conv FLOP
     (f32-equivalent; forward passes: 2 students x views + 2 teachers x views, backward =
     2x forward) against the time the MFMA pipe would need at the precision's peaks
-    (2xfp16: forwards at the 3-product peak, gradients at the 6-product one)."""
+    (2xfp16: the forwards and the 3x3 gradients at the 3-product peak, the 1x1 gradients
+    at the 6-product one, where they run; the stem and heads counted at the split peaks)."""
     F = forward_flops(cfg["S"], cfg["K"], cfg["res"]) * B
+    F3 = forward_flops(cfg["S"], cfg["K"], cfg["res"], ks=3) * B
     views = 1 if cfg["project"] == "DualPose_UBPL" else 2
     fwd, bwd = 2 * views * F + 2 * views * F, 2 * views * 2 * F       # students' + teachers' forwards; gradients
+    bwd3 = 2 * views * 2 * F3
     pieces = {"f32": 0, "bf16": 1, "2xfp16": 2, "6xbf16": 3}[precision]
     pf, pb = piece_peak(pieces), piece_peak(3 if pieces == 2 else pieces)
-    ideal_s = fwd / (pf * 1e12) + bwd / (pb * 1e12)
+    ideal_s = fwd / (pf * 1e12) + bwd3 / (pf * 1e12) + (bwd - bwd3) / (pb * 1e12)
     t = ms_per_step * 1e-3
     return {"flop_per_step": fwd + bwd, "tflops": round((fwd + bwd) / t / 1e12, 2),
             "step_frac": round(ideal_s / t, 4), "peak_tflops_fwd": round(pf, 1), "peak_tflops_bwd": round(pb, 1),
@@ -240,8 +256,8 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config=
     """The dominant kernel: the 3x3 conv at the config's largest 3x3 planes
     (headline: the 3x3 128->128 conv at the 64x64 planes on the input-halo kernel;
     the largest single entry of the rocprofv3 kernel summary, profiles/r0*_summary),
-    its launches at the precision's forward piece count (6xbf16: forward + data
-    gradient; 2xfp16: the forwards, whose data gradients run on 6xbf16).
+    its launches at the precision's piece count (forward + data gradient: on 2xfp16
+    both run 2 fp16 pieces, UBPL_FP16_BWD3 default).
     achieved = algorithmic FLOP per launch (2*B*Cout*Cin*9*H*W; f32-equivalent on the
     split paths) / its average standalone launch duration (HIP events around
     replayed launches, see PsaLaunches.time), vs the pieces' peak (6xbf16: 2.5 PF
@@ -251,7 +267,7 @@ def roofline(Kn, lib, T, models, emas, optims, args, batch, ms_per_step, config=
     peak = piece_peak(npieces)
     desc = "%s (3x3 conv, %d->%d ch, %dx%d planes, %s; %s; f32-equivalent FLOP/s, peak = bf16 dense / products)" % (
         roof_kernel(shape, npieces), shape[0], shape[1], shape[3], shape[4],
-        "fwd + dgrad" if npieces != 2 else "fwd", PIECE_NAME[npieces])
+        "fwd + dgrad", PIECE_NAME[npieces])
     os.environ["UBPL_MODEL_STREAMS"] = "0"
     try:
         with PsaLaunches(Kn, lib, shape, npieces) as rec, T._StepGraph.eager():
