@@ -633,7 +633,7 @@ class _Exec:
                           if stats and _FWD_EPI else None)
         ws = self.m.SW(0, name + ".weight") if stride == 1 else None
         if ws is not None and ws.npieces in (1, 2, 3) and ws.shape[1] == 1:
-            if Kn.conv1x1_split_load_ok(x, ws):
+            if Kn.conv1x1_split_load_ok(x, ws, small=self.m.conv_pieces == 2):
                 part = mkpart() if ws.npieces == 3 else None
                 return Kn.conv1x1_forward_split_load(x, ws, b, ps, ph, res=res, out=out, stat_part=part), part
             if ws.npieces in (2, 3):
@@ -777,7 +777,7 @@ class _Exec:
         backward partials or None); else dx."""
         ws = self.m.SW(1, name + ".weight")
         if ws is not None and ws.npieces in (1, 3) and ws.shape[1] == 1:
-            if Kn.conv1x1_split_load_ok(dy, ws):
+            if Kn.conv1x1_split_load_ok(dy, ws, small=self.m.conv_pieces == 2):
                 bwd, part = self.bwd_epi(*(bnb or (None, None))) if ws.npieces == 3 else (None, None)
                 y = Kn.conv1x1_forward_split_load(dy, ws, None, res=res, out=out, bwd=bwd)
                 return (y, part) if bnb is not None else y

@@ -551,12 +551,29 @@ def stem_weight_s2d_split(w, npieces=3):
 _NO_SOL = os.environ.get("UBPL_NO_SOL") == "1"      # diagnostic: every 1x1 on the exact-f32 kernels
 
 
-def conv1x1_split_load_ok(x, ws):
-    """The split-on-load 1x1 kernel (6xbf16, 2xfp16 or bf16) takes this shape and fills the chip."""
+# small=True (a model on the 2xfp16 precision): the split-load 1x1 also on grids below the chip's
+# CU count, down to this many workgroups — the smaller planes' 1x1 convs were on the exact-f32
+# kernel at 1/16 of the bf16 MFMA rate (-1 % step, profiles/r06_v8_sol_small_ab.txt); 0, and the
+# other precisions: only grids that fill the chip (ubpl_conv1x1_split_load_preferred)
+_SOL_MINWG = int(os.environ.get("UBPL_SOL_MINWG", "32"))
+
+
+def conv1x1_split_load_ok(x, ws, small=False):
+    """The split-on-load 1x1 kernel (6xbf16, 2xfp16 or bf16) takes this shape and fills the chip
+    (small: on grids of >= _SOL_MINWG workgroups)."""
     B, Cin, H, W = x.shape
-    return (not _NO_SOL and ws is not None and ws.npieces in (1, 2, 3) and ws.shape[1] == 1 and ws.shape[2] == Cin
-            and x.data_ptr() % 16 == 0
-            and bool(_lib.lib().ubpl_conv1x1_split_load_preferred(B, Cin, ws.shape[0], H * W)))
+    ok = (not _NO_SOL and ws is not None and ws.npieces in (1, 2, 3) and ws.shape[1] == 1 and ws.shape[2] == Cin
+          and x.data_ptr() % 16 == 0)
+    if not ok:
+        return False
+    if small and _SOL_MINWG > 0 and ws.npieces in (2, 3):
+        Cout, P = ws.shape[0], H * W
+        N = B * P
+        if not (Cin % 16 == 0 and Cout % 16 == 0 and P % 4 == 0 and N >= 4):
+            return False
+        bm = 128 if Cout % 128 == 0 and ((N + 255) // 256) * (Cout // 128) >= 256 else 64
+        return ((N + 255) // 256) * ((Cout + bm - 1) // bm) >= _SOL_MINWG
+    return bool(_lib.lib().ubpl_conv1x1_split_load_preferred(B, Cin, ws.shape[0], H * W))
 
 
 def _bnb(bwd):
