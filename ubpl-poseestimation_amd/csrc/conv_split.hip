@@ -2775,8 +2775,8 @@ int wgrad3_splits(int B, int Cin, int Cout, int H, int W) {
     // 128: one tap x 128 channels per n-tile; 64: one kernel row (3 taps) x 64 channels
     const int tiles = cb == 128 ? 9 * (Cin / cb) * (Cout / cb) : 3 * (Cin / 64) * (Cout / 64);
     const int steps = B * H * (W / 16);
-    static const int wgs = sol_env("UBPL_WGRAD3_WGS", 512);   // (tuning hook: the grid's target size)
-    int s = wgs / tiles;                               // one round of 2 workgroups per CU, not one over
+    static const int wgs = sol_env("UBPL_WGRAD3_WGS", 512);   // two workgroups per CU (256: even within noise, round 6)
+    int s = wgs / tiles;                               // whole rounds of the CUs, not one over
     if (s < 1) s = 1;
     if (s > steps / 8) s = steps / 8 > 0 ? steps / 8 : 1;   // >= 8 K steps per split
     const int per = (steps + s - 1) / s;
@@ -2891,8 +2891,8 @@ bool wgrad1_sol_supported(int B, int Cin, int Cout, int P) {
 int wgrad1_sol_splits(int B, int Cin, int Cout, int P) {
     const int tiles = (Cin / wgrad1_cb(Cin)) * (Cout / wgrad1_cb(Cout));
     const int steps = B * (P / 16);
-    static const int wgs = sol_env("UBPL_WGRAD1_WGS", 512);   // (tuning hook: the grid's target size)
-    int s = wgs / tiles;                                    // one round of 2 workgroups per CU
+    static const int wgs = sol_env("UBPL_WGRAD1_WGS", 256);   // one workgroup per CU (profiles/r06_v10_wgrad_wgs_ab.txt)
+    int s = wgs / tiles;                                    // whole rounds of the CUs
     if (s < 1) s = 1;
     if (s > steps / 8) s = steps / 8 > 0 ? steps / 8 : 1;   // >= 8 K steps per split
     const int per = (steps + s - 1) / s;
